@@ -1,0 +1,154 @@
+"""CHRONOS-MI355X headline benchmark: syscall-chains/sec analyzed + p50 verdict latency, Llama-3-8B TP=1.
+
+Metric / config from BASELINE.json.  Each rank (one per GPU, launched by torch.distributed.run for N > 1) runs an
+independent Brain engine — the DP-replica deployment of SURVEY.md §2.5 — on its own share of the sensor streams:
+
+  step = ``--streams`` kill chains arrive together (one per sensor stream); each chain's prompt is built byte-for-byte
+         with the reference template (chronos_sensor.py:109-114) from synthetic fleet telemetry run through the
+         in-kernel filter + chain tracker; the engine prefills them, decodes a schema-constrained JSON verdict
+         (<= --num-predict tokens, the reference's ~60-token replies) for every chain, detokenizes and the verdict
+         is parsed with json.loads, exactly as the sensor does (chronos_sensor.py:120).
+
+Weights are random-init Llama-3-8B (real architecture, bf16, no checkpoint offline); data is synthetic telemetry.
+Work per GPU is fixed as N grows (weak scaling).  Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=4)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--streams", type=int, default=512, help="concurrent sensor streams (chains per step) per GPU")
+    ap.add_argument("--num-predict", type=int, default=64)
+    ap.add_argument("--single-stream", type=int, default=8, help="chains for the single-stream p50 latency")
+    ap.add_argument("--burst", type=int, default=8)
+    ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--device", default="cuda")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    cuda = a.device == "cuda"
+    if cuda:
+        torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl" if cuda else "gloo")
+    device = torch.device(f"cuda:{local}" if cuda else "cpu")
+
+    from chronos.brain.engine.engine import Engine, EngineConfig
+    from chronos.sensor.prompt import VERDICT_SCHEMA, build_prompt
+    from chronos.sensor.replay import synthetic_chains
+
+    cfg = EngineConfig(model=a.model, device=str(device), max_slots=a.streams, max_model_len=512,
+                       default_num_predict=a.num_predict, decode_burst=a.burst, use_graphs=not a.no_graphs,
+                       seed=0)
+    eng = Engine(cfg)
+    total_steps = a.warmup + a.steps
+    chains = synthetic_chains(a.streams * total_steps + a.single_stream, seed=1000 + rank)
+    prompts = [build_prompt(c.history) for c in chains]
+
+    def run_step(batch):
+        reqs = [eng.submit(p, fmt=VERDICT_SCHEMA, num_predict=a.num_predict) for p in batch]
+        eng.run_until_idle()
+        return reqs
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        if cuda:
+            torch.cuda.synchronize()
+
+    for s in range(a.warmup):
+        run_step(prompts[s * a.streams:(s + 1) * a.streams])
+    barrier()
+    t0 = time.perf_counter()
+    timed = []
+    for s in range(a.warmup, total_steps):
+        timed += run_step(prompts[s * a.streams:(s + 1) * a.streams])
+    barrier()
+    elapsed = time.perf_counter() - t0
+
+    ok = 0
+    for r in timed:
+        try:
+            v = json.loads(r.text)
+            ok += int(isinstance(v, dict) and {"risk_score", "verdict", "reason"} <= set(v))
+        except Exception:
+            pass
+    lat = [r.latency for r in timed]
+    gen_tok = sum(len(r.out_ids) for r in timed)
+    prompt_tok = sum(len(r.prompt_ids) for r in timed)
+
+    # single-stream latency (the reference's regime: one chain in flight)
+    single = []
+    for p in prompts[a.streams * total_steps:]:
+        single += run_step([p])
+    single_lat = [r.latency for r in single[1:]] or [r.latency for r in single]
+
+    stats = dict(elapsed=elapsed, ok=ok, n=len(timed), lat=lat, gen=gen_tok, ptok=prompt_tok, single=single_lat)
+    if world > 1:
+        allst = [None] * world
+        dist.all_gather_object(allst, stats)
+    else:
+        allst = [stats]
+    if rank == 0:
+        t = max(s["elapsed"] for s in allst)
+        n = sum(s["n"] for s in allst)
+        oks = sum(s["ok"] for s in allst)
+        lats = [x for s in allst for x in s["lat"]]
+        singles = [x for s in allst for x in s["single"]]
+        chains_s = n / t
+        out = {
+            "metric": "syscall-chains/sec analyzed + p50 verdict latency, Llama-3-8B TP=1",
+            "value": round(chains_s, 3),
+            "unit": "chains/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1000 * t / a.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic syscall-chain telemetry (reference prompt template), random-init weights",
+            "config": {
+                "model": a.model, "global_batch": a.streams * world, "seq_len": 512,
+                "parallelism": f"dp{world}" if world > 1 else "tp1",
+                "streams_per_gpu": a.streams, "num_predict": a.num_predict,
+                "format": "verdict JSON schema (constrained decode)",
+            },
+            "p50_verdict_latency_ms": round(1000 * statistics.median(lats), 2),
+            "p99_verdict_latency_ms": round(1000 * sorted(lats)[int(0.99 * (len(lats) - 1))], 2),
+            "single_stream_p50_latency_ms": round(1000 * statistics.median(singles), 2) if singles else None,
+            "verdicts_valid": f"{oks}/{n}",
+            "prompt_tokens_per_chain": round(sum(s["ptok"] for s in allst) / n, 1),
+            "verdict_tokens_per_chain": round(sum(s["gen"] for s in allst) / n, 1),
+            "generated_tokens_per_s": round(sum(s["gen"] for s in allst) / t, 1),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

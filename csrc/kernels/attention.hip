@@ -1,0 +1,299 @@
+// attention.hip — paged GQA attention for prefill (chunked, causal, varlen) and decode.
+//
+// One kernel serves both phases.  Work item = (q tile, kv head, kv split):
+//   * a q tile is NQT x 16 "rows"; row R = (token rel0 + R / G, q head h*G + R % G), G = Hq / Hkv.  All rows of a tile
+//     share one kv head, so every K/V byte a workgroup loads feeds G query heads (GQA reuse in registers).
+//   * the 4 waves of a workgroup split the tile's kv range in interleaved 32-token steps; each keeps its own online
+//     softmax state and the four are merged through LDS at the end.  Long contexts additionally split the kv range
+//     over workgroups (grid.z) and a combine kernel merges the partial (O, lse) pairs (flash-decoding).
+//
+// MFMA mapping (v_mfma_f32_16x16x32_bf16, cdna_hip_programming.md §3 operand maps):
+//   S^T[16 tok][16 rows] = K[16 tok][128] · Q^T  — "swapped" QK^T, 4 MFMAs per 16 tokens (K chunk of 32 dims each).
+//       A = K rows straight from the cache (k_cache[blk][h][tok][128], 16 B per lane), B = Q^T fragments in VGPRs.
+//       Result: lane l holds S^T[tok 4(l>>4)+i][row l&15] — the query row is the lane, so the row max/sum needs only
+//       two xor-shuffles (16, 32) and P never leaves registers.
+//   O^T[16 dims][16 rows] += V^T[16 dims][32 tok] · P^T[32 tok][16 rows] — 8 MFMAs per 32 tokens.
+//       The k (token) order inside the MFMA is permuted identically on both operands: k = 8h + j <-> token
+//       4h + j (j < 4) or 16 + 4h + (j - 4) (j >= 4), which is exactly where the S^T accumulator left P.  V is cached
+//       transposed (v_cache[blk][h][dim][tok]) so the A fragment is two 8-byte row reads.
+//
+// Masking: keys > the row's position (causal) or >= the split end get score -inf; rows with no key yield 0.  V lanes
+// of keys past the split end are zeroed so stale cache bytes can never reach the accumulator (p = 0 * NaN guard).
+#include "chronos_hip.h"
+
+namespace chronos {
+
+constexpr int kD = 128;
+constexpr int kOStride = 132;  // LDS row stride (floats) of the merge buffer: breaks the 512-B row bank aliasing
+
+template <int NQT>
+__global__ void __launch_bounds__(256) paged_attn_kernel(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
+    const int32_t* __restrict__ block_table, int bt_stride, const int32_t* __restrict__ q_start,
+    const int32_t* __restrict__ ctx_len, const int32_t* __restrict__ tiles, uint16_t* __restrict__ out,
+    float* __restrict__ part_o, float* __restrict__ part_lse, int hq, int hkv, int block_size, float scale_log2) {
+    constexpr int ROWS = NQT * 16;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float* sm = smem;                 // [4][ROWS]
+    float* sl = sm + 4 * ROWS;        // [4][ROWS]
+    float* so = sl + 4 * ROWS;        // [4][ROWS][kOStride]
+
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r = lane & 15, h4 = lane >> 4;
+    const int G = hq / hkv;
+    const int h = blockIdx.y;
+    const int tile = blockIdx.x;
+    const int nsplit = gridDim.z;
+
+    int seq, rel0, qbase, qlen;
+    if (tiles) {
+        seq = tiles[2 * tile];
+        rel0 = tiles[2 * tile + 1];
+        qbase = q_start[seq];
+        qlen = q_start[seq + 1] - qbase;
+    } else {  // decode: tile i = sequence i, one query token each
+        seq = tile;
+        rel0 = 0;
+        qbase = tile;
+        qlen = 1;
+    }
+    const int ctx = ctx_len[seq];
+    const int ctx0 = ctx - qlen;  // position of the first query token of this sequence's chunk
+
+    int rpos[NQT];
+    bf16x8 qf[NQT][4];
+#pragma unroll
+    for (int qt = 0; qt < NQT; ++qt) {
+        const int R = qt * 16 + r;
+        const int tr = rel0 + R / G, hd = h * G + R % G;
+        const bool valid = tr < qlen;
+        rpos[qt] = valid ? ctx0 + tr : -1;
+        const uint16_t* qp = q + ((int64_t)(qbase + (valid ? tr : 0)) * hq + hd) * kD + 8 * h4;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            bf16x8 v = *reinterpret_cast<const bf16x8*>(qp + 32 * c);
+            if (!valid) v = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+            qf[qt][c] = v;
+        }
+    }
+    int last_tr = rel0 + ROWS / G - 1;
+    if (last_tr > qlen - 1) last_tr = qlen - 1;
+    const int kv_end = ctx0 + last_tr + 1;
+    int chunk = (kv_end + nsplit - 1) / nsplit;
+    chunk = (chunk + 31) & ~31;
+    const int ks = blockIdx.z * chunk;
+    const int ke = min(kv_end, ks + chunk);
+
+    float m[NQT], lsum[NQT];
+    f32x4 o[NQT][8];
+#pragma unroll
+    for (int qt = 0; qt < NQT; ++qt) {
+        m[qt] = -1e30f;
+        lsum[qt] = 0.f;
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) o[qt][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    const int32_t* bt = block_table + (int64_t)seq * bt_stride;
+
+    for (int t0 = ks + w * 32; t0 < ke; t0 += 128) {
+        bf16x8 kf[2][4];
+        bf16x4 vf[2][8];
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            const int tg = t0 + 16 * g;
+            if (tg < ke) {
+                const int64_t blk = bt[tg / block_size];
+                const int off = tg % block_size;
+                const uint16_t* kp = kc + (((blk * hkv + h) * block_size) + off + r) * kD + 8 * h4;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) kf[g][c] = *reinterpret_cast<const bf16x8*>(kp + 32 * c);
+                const uint16_t* vp = vc + ((blk * hkv + h) * kD) * (int64_t)block_size + off + 4 * h4;
+#pragma unroll
+                for (int dt = 0; dt < 8; ++dt)
+                    vf[g][dt] = *reinterpret_cast<const bf16x4*>(vp + (int64_t)(dt * 16 + r) * block_size);
+            } else {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) kf[g][c] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+                for (int dt = 0; dt < 8; ++dt) vf[g][dt] = bf16x4{0, 0, 0, 0};
+            }
+        }
+        if (t0 + 32 > ke) {  // partial step: zero V of keys past the end (uniform branch)
+#pragma unroll
+            for (int g = 0; g < 2; ++g)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (t0 + 16 * g + 4 * h4 + i >= ke)
+#pragma unroll
+                        for (int dt = 0; dt < 8; ++dt) vf[g][dt][i] = (__bf16)0.f;
+        }
+#pragma unroll
+        for (int qt = 0; qt < NQT; ++qt) {
+            f32x4 s[2];
+#pragma unroll
+            for (int g = 0; g < 2; ++g) {
+                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int c = 0; c < 4; ++c) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[g][c], qf[qt][c], acc, 0, 0, 0);
+                s[g] = acc;
+            }
+            float mx = -INFINITY;
+#pragma unroll
+            for (int g = 0; g < 2; ++g)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const int tok = t0 + 16 * g + 4 * h4 + i;
+                    float v = s[g][i] * scale_log2;
+                    if (tok >= ke || tok > rpos[qt]) v = -INFINITY;
+                    s[g][i] = v;
+                    mx = fmaxf(mx, v);
+                }
+            mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+            const float mnew = fmaxf(m[qt], mx);
+            const float alpha = exp2f(m[qt] - mnew);
+            m[qt] = mnew;
+            float ps = 0.f;
+            bf16x8 pf;
+#pragma unroll
+            for (int g = 0; g < 2; ++g)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float p = exp2f(s[g][i] - mnew);
+                    ps += p;
+                    pf[4 * g + i] = (__bf16)p;
+                }
+            lsum[qt] = lsum[qt] * alpha + ps;
+#pragma unroll
+            for (int dt = 0; dt < 8; ++dt) {
+                o[qt][dt] *= alpha;
+                const bf16x8 va = __builtin_shufflevector(vf[0][dt], vf[1][dt], 0, 1, 2, 3, 4, 5, 6, 7);
+                o[qt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pf, o[qt][dt], 0, 0, 0);
+            }
+        }
+    }
+
+    // ---- merge the four waves' (m, l, O) through LDS -----------------------------------------------------------
+#pragma unroll
+    for (int qt = 0; qt < NQT; ++qt) {
+        float lt = lsum[qt];
+        lt += __shfl_xor(lt, 16, 64);
+        lt += __shfl_xor(lt, 32, 64);
+        const int row = qt * 16 + r;
+        if (h4 == 0) {
+            sm[w * ROWS + row] = m[qt];
+            sl[w * ROWS + row] = lt;
+        }
+        float* orow = so + (w * ROWS + row) * kOStride;
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) *reinterpret_cast<f32x4*>(orow + dt * 16 + 4 * h4) = o[qt][dt];
+    }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < ROWS * 16; idx += 256) {
+        const int row = idx >> 4, c8 = idx & 15;
+        const int tr = rel0 + row / G, hd = h * G + row % G;
+        if (tr >= qlen) continue;
+        float M = -1e30f;
+#pragma unroll
+        for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, sm[ww * ROWS + row]);
+        float L = 0.f, acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int ww = 0; ww < 4; ++ww) {
+            const float f = exp2f(sm[ww * ROWS + row] - M);
+            L += sl[ww * ROWS + row] * f;
+            const float* orow = so + (ww * ROWS + row) * kOStride + c8 * 8;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[j] += orow[j] * f;
+        }
+        const float inv = L > 0.f ? 1.f / L : 0.f;
+        if (nsplit == 1) {
+            u16x8 ov;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) ov[j] = f2bf(acc[j] * inv);
+            *reinterpret_cast<u16x8*>(out + ((int64_t)(qbase + tr) * hq + hd) * kD + c8 * 8) = ov;
+        } else {
+            const int64_t prow = (((int64_t)blockIdx.z * gridDim.x + tile) * hkv + h) * ROWS + row;
+            float* po = part_o + prow * kD + c8 * 8;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) po[j] = acc[j] * inv;
+            if (c8 == 0) part_lse[prow] = L > 0.f ? M + __log2f(L) : -INFINITY;
+        }
+    }
+}
+
+// Flash-decoding combine: out = sum_s 2^(lse_s - M) O_s / sum_s 2^(lse_s - M).
+template <int NQT>
+__global__ void __launch_bounds__(256) paged_attn_combine_kernel(
+    const float* __restrict__ part_o, const float* __restrict__ part_lse, const int32_t* __restrict__ q_start,
+    const int32_t* __restrict__ tiles, uint16_t* __restrict__ out, int hq, int hkv, int nsplit, int ntiles) {
+    constexpr int ROWS = NQT * 16;
+    const int tile = blockIdx.x, h = blockIdx.y, G = hq / hkv;
+    int rel0, qbase, qlen;
+    if (tiles) {
+        const int seq = tiles[2 * tile];
+        rel0 = tiles[2 * tile + 1];
+        qbase = q_start[seq];
+        qlen = q_start[seq + 1] - qbase;
+    } else {
+        rel0 = 0;
+        qbase = tile;
+        qlen = 1;
+    }
+    for (int idx = threadIdx.x; idx < ROWS * 16; idx += 256) {
+        const int row = idx >> 4, c8 = idx & 15;
+        const int tr = rel0 + row / G, hd = h * G + row % G;
+        if (tr >= qlen) continue;
+        float M = -INFINITY;
+        for (int s = 0; s < nsplit; ++s)
+            M = fmaxf(M, part_lse[(((int64_t)s * ntiles + tile) * hkv + h) * ROWS + row]);
+        float L = 0.f, acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (M > -INFINITY) {
+            for (int s = 0; s < nsplit; ++s) {
+                const int64_t prow = (((int64_t)s * ntiles + tile) * hkv + h) * ROWS + row;
+                const float f = exp2f(part_lse[prow] - M);
+                if (f == 0.f) continue;
+                L += f;
+                const float* po = part_o + prow * kD + c8 * 8;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc[j] += po[j] * f;
+            }
+        }
+        const float inv = L > 0.f ? 1.f / L : 0.f;
+        u16x8 ov;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ov[j] = f2bf(acc[j] * inv);
+        *reinterpret_cast<u16x8*>(out + ((int64_t)(qbase + tr) * hq + hd) * kD + c8 * 8) = ov;
+    }
+}
+
+size_t paged_attn_smem(int nqt) { return (size_t)(8 * nqt * 16 + 4 * nqt * 16 * kOStride) * sizeof(float); }
+
+void launch_paged_attn(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* block_table,
+                       int bt_stride, const int32_t* q_start, const int32_t* ctx_len, const int32_t* tiles,
+                       int ntiles, int nqt, int nsplit, uint16_t* out, float* part_o, float* part_lse, int hq,
+                       int hkv, int block_size, float scale, hipStream_t st) {
+    if (ntiles == 0) return;
+    const float scale_log2 = scale * 1.4426950408889634f;
+    const dim3 grid(ntiles, hkv, nsplit), block(256);
+    const size_t sh = paged_attn_smem(nqt);
+    if (nqt == 1) {
+        hipLaunchKernelGGL(paged_attn_kernel<1>, grid, block, sh, st, q, kc, vc, block_table, bt_stride, q_start,
+                           ctx_len, tiles, out, part_o, part_lse, hq, hkv, block_size, scale_log2);
+        if (nsplit > 1)
+            hipLaunchKernelGGL(paged_attn_combine_kernel<1>, dim3(ntiles, hkv), block, 0, st, part_o, part_lse,
+                               q_start, tiles, out, hq, hkv, nsplit, ntiles);
+    } else {
+        static bool attr = [] {  // > 64 KiB dynamic LDS needs the opt-in (gfx950 has 160 KiB per CU)
+            return hipFuncSetAttribute((const void*)paged_attn_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)paged_attn_smem(2)) == hipSuccess;
+        }();
+        (void)attr;
+        hipLaunchKernelGGL(paged_attn_kernel<2>, grid, block, sh, st, q, kc, vc, block_table, bt_stride, q_start,
+                           ctx_len, tiles, out, part_o, part_lse, hq, hkv, block_size, scale_log2);
+        if (nsplit > 1)
+            hipLaunchKernelGGL(paged_attn_combine_kernel<2>, dim3(ntiles, hkv), block, 0, st, part_o, part_lse,
+                               q_start, tiles, out, hq, hkv, nsplit, ntiles);
+    }
+}
+
+}  // namespace chronos

@@ -1,0 +1,234 @@
+// bindings.cpp — registers the gfx950 HIP kernels as torch operators (torch.ops.chronos.*).
+//
+// Every op checks dtype/shape/contiguity on the host BEFORE launching (a bad launch geometry on a hand-written kernel
+// can fault the whole GPU box), launches on the current HIP stream (so ops are hipGraph-capturable), and never
+// allocates inside a captured region except through torch's caching allocator.
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+#include <torch/library.h>
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace chronos {
+void launch_embedding(const int32_t*, const uint16_t*, uint16_t*, int, int, int64_t, int64_t, hipStream_t);
+void launch_rmsnorm(const uint16_t*, uint16_t*, const uint16_t*, uint16_t*, int, int, float, hipStream_t);
+void launch_rope_kv_write(const uint16_t*, const int32_t*, const int32_t*, const int32_t*, int, const float*,
+                          uint16_t*, uint16_t*, uint16_t*, int, int, int, int, int, hipStream_t);
+void launch_silu_mul(const uint16_t*, uint16_t*, int64_t, int, hipStream_t);
+size_t paged_attn_smem(int nqt);
+void launch_paged_attn(const uint16_t*, const uint16_t*, const uint16_t*, const int32_t*, int, const int32_t*,
+                       const int32_t*, const int32_t*, int, int, int, uint16_t*, float*, float*, int, int, int, float,
+                       hipStream_t);
+void launch_constrained_sample(const void*, bool, int64_t, const int32_t*, int, int, const int16_t*, const int16_t*,
+                               int, int32_t*, int32_t*, const float*, const int32_t*, int32_t*, int32_t*, int32_t*,
+                               int32_t*, int32_t*, int, hipStream_t);
+}  // namespace chronos
+
+namespace {
+
+using at::Tensor;
+
+inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+inline const uint16_t* bf(const Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
+inline uint16_t* bfm(const Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
+inline const int32_t* i32(const Tensor& t) { return t.data_ptr<int32_t>(); }
+inline int32_t* i32m(const Tensor& t) { return t.data_ptr<int32_t>(); }
+
+#define CHK(c, msg) TORCH_CHECK((c), "chronos: ", msg)
+inline void chk_gpu(const Tensor& t, const char* n) {
+    CHK(t.is_cuda(), std::string(n) + " must be a GPU tensor");
+    CHK(t.is_contiguous(), std::string(n) + " must be contiguous");
+}
+inline void chk_bf16(const Tensor& t, const char* n) {
+    chk_gpu(t, n);
+    CHK(t.scalar_type() == at::kBFloat16, std::string(n) + " must be bfloat16");
+}
+inline void chk_i32(const Tensor& t, const char* n) {
+    chk_gpu(t, n);
+    CHK(t.scalar_type() == at::kInt, std::string(n) + " must be int32");
+}
+
+Tensor embedding(const Tensor& ids, const Tensor& table, int64_t vstart) {
+    chk_i32(ids, "ids");
+    chk_bf16(table, "table");
+    CHK(table.dim() == 2 && table.size(1) % 8 == 0, "table must be [V, d] with d % 8 == 0");
+    c10::hip::HIPGuard g(ids.device());
+    auto out = at::empty({ids.numel(), table.size(1)}, table.options());
+    chronos::launch_embedding(i32(ids), bf(table), bfm(out), (int)ids.numel(), (int)table.size(1), vstart,
+                              table.size(0), cur_stream());
+    return out;
+}
+
+Tensor rmsnorm(const Tensor& x, const Tensor& w, double eps) {
+    chk_bf16(x, "x");
+    chk_bf16(w, "w");
+    const int64_t d = x.size(-1);
+    CHK(w.numel() == d && d % 8 == 0 && d <= 16384, "rmsnorm: d must match w, be % 8 and <= 16384");
+    c10::hip::HIPGuard g(x.device());
+    auto y = at::empty_like(x);
+    chronos::launch_rmsnorm(bf(x), nullptr, bf(w), bfm(y), (int)(x.numel() / d), (int)d, (float)eps, cur_stream());
+    return y;
+}
+
+// resid <- bf16(x + resid); returns rmsnorm(resid) * w
+Tensor add_rmsnorm(const Tensor& x, const Tensor& resid, const Tensor& w, double eps) {
+    chk_bf16(x, "x");
+    chk_bf16(resid, "resid");
+    chk_bf16(w, "w");
+    const int64_t d = x.size(-1);
+    CHK(resid.sizes() == x.sizes(), "add_rmsnorm: shape mismatch");
+    CHK(w.numel() == d && d % 8 == 0 && d <= 16384, "add_rmsnorm: d must match w, be % 8 and <= 16384");
+    c10::hip::HIPGuard g(x.device());
+    auto y = at::empty_like(x);
+    chronos::launch_rmsnorm(bf(x), bfm(resid), bf(w), bfm(y), (int)(x.numel() / d), (int)d, (float)eps, cur_stream());
+    return y;
+}
+
+void rope_kv_write(const Tensor& qkv, const Tensor& pos, const Tensor& tok_seq, const Tensor& block_table,
+                   const Tensor& cos_sin, const Tensor& q_out, const Tensor& k_cache, const Tensor& v_cache, int64_t hq,
+                   int64_t hkv, bool write_q) {
+    chk_bf16(qkv, "qkv");
+    chk_i32(pos, "pos");
+    chk_i32(tok_seq, "tok_seq");
+    chk_i32(block_table, "block_table");
+    chk_gpu(cos_sin, "cos_sin");
+    CHK(cos_sin.scalar_type() == at::kFloat && cos_sin.dim() == 2 && cos_sin.size(1) == 128, "cos_sin [P,128] f32");
+    chk_bf16(q_out, "q_out");
+    chk_bf16(k_cache, "k_cache");
+    chk_bf16(v_cache, "v_cache");
+    const int64_t t = qkv.size(0);
+    CHK(qkv.dim() == 2 && qkv.size(1) == (hq + 2 * hkv) * 128, "qkv must be [T, (hq+2hkv)*128]");
+    CHK(pos.numel() == t && tok_seq.numel() == t, "pos/tok_seq must have T entries");
+    CHK(!write_q || q_out.numel() >= t * hq * 128, "q_out too small");
+    CHK(k_cache.dim() == 4 && k_cache.size(1) == hkv && k_cache.size(3) == 128, "k_cache [NB, hkv, BS, 128]");
+    CHK(v_cache.dim() == 4 && v_cache.size(1) == hkv && v_cache.size(2) == 128 && v_cache.size(3) == k_cache.size(2),
+        "v_cache [NB, hkv, 128, BS]");
+    CHK(block_table.dim() == 2, "block_table [B, max_blocks]");
+    c10::hip::HIPGuard g(qkv.device());
+    chronos::launch_rope_kv_write(bf(qkv), i32(pos), i32(tok_seq), i32(block_table), (int)block_table.size(1),
+                                  cos_sin.data_ptr<float>(), bfm(q_out), bfm(k_cache), bfm(v_cache), (int)t, (int)hq,
+                                  (int)hkv, (int)k_cache.size(2), write_q ? 1 : 0, cur_stream());
+}
+
+Tensor silu_mul(const Tensor& gu) {
+    chk_bf16(gu, "gate_up");
+    const int64_t f2 = gu.size(-1);
+    CHK(f2 % 16 == 0, "gate_up last dim must be 2F with F % 8 == 0");
+    c10::hip::HIPGuard g(gu.device());
+    auto sizes = gu.sizes().vec();
+    sizes.back() = f2 / 2;
+    auto out = at::empty(sizes, gu.options());
+    chronos::launch_silu_mul(bf(gu), bfm(out), gu.numel() / f2, (int)(f2 / 2), cur_stream());
+    return out;
+}
+
+Tensor paged_attention(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_table,
+                       const Tensor& q_start, const Tensor& ctx_len, const c10::optional<Tensor>& tiles,
+                       int64_t ntiles, int64_t nqt, int64_t nsplit, double scale) {
+    chk_bf16(q, "q");
+    chk_bf16(k_cache, "k_cache");
+    chk_bf16(v_cache, "v_cache");
+    chk_i32(block_table, "block_table");
+    chk_i32(q_start, "q_start");
+    chk_i32(ctx_len, "ctx_len");
+    CHK(q.dim() == 3 && q.size(2) == 128, "q must be [T, Hq, 128]");
+    const int64_t hq = q.size(1), hkv = k_cache.size(1), bs = k_cache.size(2);
+    CHK(hq % hkv == 0 && 16 % (hq / hkv) == 0, "GQA group Hq/Hkv must divide 16");
+    CHK(bs % 16 == 0, "block size must be a multiple of 16");
+    CHK(v_cache.size(2) == 128 && v_cache.size(3) == bs, "v_cache [NB, hkv, 128, BS]");
+    CHK(nqt == 1 || nqt == 2, "nqt must be 1 or 2");
+    CHK(nsplit >= 1 && nsplit <= 256, "nsplit in [1, 256]");
+    const int32_t* tp = nullptr;
+    if (tiles.has_value()) {
+        chk_i32(*tiles, "tiles");
+        CHK(tiles->numel() >= 2 * ntiles, "tiles must be [ntiles, 2]");
+        tp = i32(*tiles);
+    } else {
+        CHK(ctx_len.numel() >= ntiles && q.size(0) >= ntiles, "decode mode: one query token per tile");
+    }
+    c10::hip::HIPGuard g(q.device());
+    auto out = at::empty_like(q);
+    Tensor po, pl;
+    if (nsplit > 1) {
+        const int64_t rows = nsplit * ntiles * hkv * nqt * 16;
+        po = at::empty({rows, 128}, q.options().dtype(at::kFloat));
+        pl = at::empty({rows}, q.options().dtype(at::kFloat));
+    }
+    chronos::launch_paged_attn(bf(q), bf(k_cache), bf(v_cache), i32(block_table), (int)block_table.size(1),
+                               i32(q_start), i32(ctx_len), tp, (int)ntiles, (int)nqt, (int)nsplit, bfm(out),
+                               nsplit > 1 ? po.data_ptr<float>() : nullptr, nsplit > 1 ? pl.data_ptr<float>() : nullptr,
+                               (int)hq, (int)hkv, (int)bs, (float)scale, cur_stream());
+    return out;
+}
+
+void constrained_sample(const Tensor& logits, const c10::optional<Tensor>& row_of_slot, const Tensor& next,
+                        const Tensor& dist, int64_t done_state, const Tensor& state, const Tensor& remaining,
+                        const c10::optional<Tensor>& temperature, const c10::optional<Tensor>& seed, const Tensor& ids,
+                        const Tensor& pos, const Tensor& ctx, const Tensor& nout, const Tensor& out_tokens) {
+    CHK(logits.is_cuda() && logits.dim() == 2 && logits.stride(1) == 1, "logits [rows, V] row-contiguous");
+    CHK(logits.scalar_type() == at::kBFloat16 || logits.scalar_type() == at::kFloat, "logits bf16 or f32");
+    chk_gpu(next, "next");
+    CHK(next.scalar_type() == at::kShort && next.dim() == 2, "next must be int16 [S, V]");
+    CHK(dist.scalar_type() == at::kShort && dist.numel() == next.size(0), "dist must be int16 [S]");
+    const int64_t vocab = next.size(1);
+    CHK(logits.size(1) >= vocab, "logits narrower than the DFA vocabulary");
+    chk_i32(state, "state");
+    const int64_t n = state.numel();
+    for (const Tensor* t : {&remaining, &ids, &pos, &ctx, &nout}) {
+        chk_i32(*t, "slot tensor");
+        CHK(t->numel() >= n, "slot tensors must have one entry per slot");
+    }
+    chk_i32(out_tokens, "out_tokens");
+    CHK(out_tokens.dim() == 2 && out_tokens.size(0) >= n, "out_tokens [slots, max_out]");
+    const int32_t* rp = nullptr;
+    if (row_of_slot.has_value()) {
+        chk_i32(*row_of_slot, "row_of_slot");
+        rp = i32(*row_of_slot);
+    } else {
+        CHK(logits.size(0) >= n, "one logits row per slot");
+    }
+    const float* tp = nullptr;
+    if (temperature.has_value()) {
+        chk_gpu(*temperature, "temperature");
+        CHK(temperature->scalar_type() == at::kFloat, "temperature f32");
+        tp = temperature->data_ptr<float>();
+    }
+    const int32_t* sp = nullptr;
+    if (seed.has_value()) {
+        chk_i32(*seed, "seed");
+        sp = i32(*seed);
+    }
+    c10::hip::HIPGuard g(logits.device());
+    chronos::launch_constrained_sample(logits.data_ptr(), logits.scalar_type() == at::kFloat, logits.stride(0), rp,
+                                       (int)n, (int)vocab, next.data_ptr<int16_t>(), dist.data_ptr<int16_t>(),
+                                       (int)done_state, i32m(state), i32m(remaining), tp, sp, i32m(ids), i32m(pos),
+                                       i32m(ctx), i32m(nout), i32m(out_tokens), (int)out_tokens.size(1), cur_stream());
+}
+
+}  // namespace
+
+TORCH_LIBRARY(chronos, m) {
+    m.def("embedding(Tensor ids, Tensor table, int vstart) -> Tensor");
+    m.def("rmsnorm(Tensor x, Tensor w, float eps) -> Tensor");
+    m.def("add_rmsnorm(Tensor x, Tensor(a!) resid, Tensor w, float eps) -> Tensor");
+    m.def("rope_kv_write(Tensor qkv, Tensor pos, Tensor tok_seq, Tensor block_table, Tensor cos_sin, "
+          "Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, int hq, int hkv, bool write_q) -> ()");
+    m.def("silu_mul(Tensor gate_up) -> Tensor");
+    m.def("paged_attention(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_table, Tensor q_start, "
+          "Tensor ctx_len, Tensor? tiles, int ntiles, int nqt, int nsplit, float scale) -> Tensor");
+    m.def("constrained_sample(Tensor logits, Tensor? row_of_slot, Tensor next, Tensor dist, int done_state, "
+          "Tensor(a!) state, Tensor(b!) remaining, Tensor? temperature, Tensor? seed, Tensor(c!) ids, Tensor(d!) pos, "
+          "Tensor(e!) ctx, Tensor(f!) nout, Tensor(g!) out_tokens) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(chronos, CUDA, m) {
+    m.impl("embedding", &embedding);
+    m.impl("rmsnorm", &rmsnorm);
+    m.impl("add_rmsnorm", &add_rmsnorm);
+    m.impl("rope_kv_write", &rope_kv_write);
+    m.impl("silu_mul", &silu_mul);
+    m.impl("paged_attention", &paged_attention);
+    m.impl("constrained_sample", &constrained_sample);
+}

@@ -1,0 +1,214 @@
+// elementwise.hip — memory-bound kernels of the Llama-3 block:
+//   embedding gather (vocab-parallel aware), RMSNorm with fused residual add, RoPE fused with the paged KV-cache
+//   write, SiLU(gate)*up.
+//
+// All bf16 traffic is 16 B per lane (8 elements).  Each kernel reads/writes its tensors exactly once; the residual
+// add, the norm and the KV-cache write are fused into the producer of the next GEMM's input so no intermediate round
+// trips through HBM.
+#include "chronos_hip.h"
+
+namespace chronos {
+
+// ------------------------------------------------------------------------------------------------------------------
+// K1 embedding gather.  out[t, :] = table[ids[t] - vstart, :] if vstart <= ids[t] < vstart + vrows else 0 (the
+// zero rows of a vocab-parallel shard are summed away by the TP all-reduce).
+// ------------------------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) embedding_kernel(const int32_t* __restrict__ ids, const uint16_t* __restrict__ table,
+                                                        uint16_t* __restrict__ out, int d, int64_t vstart, int64_t vrows) {
+    const int t = blockIdx.x;
+    const int64_t id = (int64_t)ids[t] - vstart;
+    const bool ok = id >= 0 && id < vrows;
+    const u16x8* src = reinterpret_cast<const u16x8*>(table + (ok ? id : 0) * (int64_t)d);
+    u16x8* dst = reinterpret_cast<u16x8*>(out + (int64_t)t * d);
+    for (int i = threadIdx.x; i < d / 8; i += blockDim.x) {
+        u16x8 v = ok ? src[i] : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        dst[i] = v;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------------------------
+// K2 RMSNorm (+ fused residual add).  One 256-thread block per row; the row is held in registers between the
+// reduction and the scaling pass (d <= 256*8*MAXV).
+//   plain:     y = x * rsqrt(mean(x^2) + eps) * w
+//   residual:  r = bf16(x + r) (written back), y = rmsnorm(r) * w       (HF Llama: residual kept in bf16)
+// ------------------------------------------------------------------------------------------------------------------
+template <int MAXV, bool RESID>
+__global__ void __launch_bounds__(256) rmsnorm_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ resid,
+                                                      const uint16_t* __restrict__ w, uint16_t* __restrict__ y, int d,
+                                                      float eps) {
+    __shared__ float red[16];
+    const int64_t row = blockIdx.x;
+    const u16x8* xv = reinterpret_cast<const u16x8*>(x + row * d);
+    u16x8* rv = reinterpret_cast<u16x8*>(resid + row * d);
+    const u16x8* wv = reinterpret_cast<const u16x8*>(w);
+    u16x8* yv = reinterpret_cast<u16x8*>(y + row * d);
+    const int nv = d / 8;
+    float vals[MAXV][8];
+    float ss = 0.f;
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+        const int i = threadIdx.x + k * 256;
+        if (i < nv) {
+            u16x8 a = xv[i];
+            if constexpr (RESID) {
+                u16x8 b = rv[i];
+                u16x8 s;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    s[j] = f2bf(bf2f(a[j]) + bf2f(b[j]));
+                    vals[k][j] = bf2f(s[j]);
+                }
+                rv[i] = s;
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) vals[k][j] = bf2f(a[j]);
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) ss += vals[k][j] * vals[k][j];
+        }
+    }
+    const float tot = block_sum(ss, red);
+    const float inv = rsqrtf(tot / (float)d + eps);
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+        const int i = threadIdx.x + k * 256;
+        if (i < nv) {
+            u16x8 g = wv[i], o;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(f2bf(vals[k][j] * inv)) * bf2f(g[j]));
+            yv[i] = o;
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------------------------
+// K4 RoPE + paged KV-cache write (+ K13 layout).  Input: the QKV GEMM output qkv[T, (Hq + 2*Hkv) * 128].
+//   q  -> q_out[T, Hq, 128]                rotated (HF rotate-half convention)
+//   k  -> k_cache[blk, h, t % BS, :]        rotated       (row-major per token: B operand of S^T = K Q^T)
+//   v  -> v_cache[blk, h, :, t % BS]        transposed    (A operand of O^T = V^T P^T, see attention.hip)
+// The cache slot is derived on device from block_table[tok_seq[t], pos / BS] so a captured decode graph needs no
+// host-side slot mapping.  cos_sin[pos, 0:64] = cos, [64:128] = sin (f32, precomputed on the host incl. Llama-3.1
+// frequency scaling).  8 threads per head, each owning dims {8i..8i+7} and {64+8i..64+8i+7}.
+// ------------------------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) rope_kv_write_kernel(
+    const uint16_t* __restrict__ qkv, const int32_t* __restrict__ pos, const int32_t* __restrict__ tok_seq,
+    const int32_t* __restrict__ block_table, int bt_stride, const float* __restrict__ cos_sin,
+    uint16_t* __restrict__ q_out, uint16_t* __restrict__ k_cache, uint16_t* __restrict__ v_cache, int hq, int hkv,
+    int block_size, int write_q) {
+    constexpr int D = 128;
+    const int t = blockIdx.x;
+    const int unit = blockIdx.y * 32 + (threadIdx.x >> 3);  // head index over [q heads | k heads | v heads]
+    const int i = threadIdx.x & 7;
+    const int nh = hq + 2 * hkv;
+    if (unit >= nh) return;
+    const int p = pos[t];
+    const uint16_t* src = qkv + ((int64_t)t * nh + unit) * D;
+    const int seq = tok_seq[t];
+    const int64_t blk = block_table[(int64_t)seq * bt_stride + p / block_size];
+    const int off = p % block_size;
+    if (unit < hq + hkv) {
+        if (unit < hq && !write_q) return;
+        const u16x8 a = *reinterpret_cast<const u16x8*>(src + 8 * i);
+        const u16x8 b = *reinterpret_cast<const u16x8*>(src + 64 + 8 * i);
+        const float* cs = cos_sin + (int64_t)p * D;
+        const float4 c0 = *reinterpret_cast<const float4*>(cs + 8 * i);
+        const float4 c1 = *reinterpret_cast<const float4*>(cs + 8 * i + 4);
+        const float4 s0 = *reinterpret_cast<const float4*>(cs + 64 + 8 * i);
+        const float4 s1 = *reinterpret_cast<const float4*>(cs + 64 + 8 * i + 4);
+        const float c[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+        const float s[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+        u16x8 ra, rb;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float x1 = bf2f(a[j]), x2 = bf2f(b[j]);
+            ra[j] = f2bf(x1 * c[j] - x2 * s[j]);
+            rb[j] = f2bf(x2 * c[j] + x1 * s[j]);
+        }
+        uint16_t* dst;
+        if (unit < hq) {
+            dst = q_out + ((int64_t)t * hq + unit) * D;
+        } else {
+            const int h = unit - hq;
+            dst = k_cache + (((blk * hkv + h) * block_size) + off) * D;
+        }
+        *reinterpret_cast<u16x8*>(dst + 8 * i) = ra;
+        *reinterpret_cast<u16x8*>(dst + 64 + 8 * i) = rb;
+    } else {
+        const int h = unit - hq - hkv;
+        const u16x8 a = *reinterpret_cast<const u16x8*>(src + 16 * i);
+        const u16x8 b = *reinterpret_cast<const u16x8*>(src + 16 * i + 8);
+        uint16_t* dst = v_cache + ((blk * hkv + h) * D) * (int64_t)block_size + off;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            dst[(int64_t)(16 * i + j) * block_size] = a[j];
+            dst[(int64_t)(16 * i + 8 + j) * block_size] = b[j];
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------------------------------
+// K9 SwiGLU: out[t, f] = silu(gu[t, f]) * gu[t, F + f]
+// ------------------------------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) silu_mul_kernel(const uint16_t* __restrict__ gu, uint16_t* __restrict__ out,
+                                                       int64_t rows, int f) {
+    const int nv = f / 8;
+    const int64_t total = rows * nv;
+    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = idx / nv;
+        const int c = (int)(idx - r * nv);
+        const u16x8 g = reinterpret_cast<const u16x8*>(gu + r * 2 * f)[c];
+        const u16x8 u = reinterpret_cast<const u16x8*>(gu + r * 2 * f + f)[c];
+        u16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const float x = bf2f(g[j]);
+            const float sx = bf2f(f2bf(x / (1.f + __expf(-x))));
+            o[j] = f2bf(sx * bf2f(u[j]));
+        }
+        reinterpret_cast<u16x8*>(out + r * f)[c] = o;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------------------------
+// Host launchers (called from bindings.cpp)
+// ------------------------------------------------------------------------------------------------------------------
+void launch_embedding(const int32_t* ids, const uint16_t* table, uint16_t* out, int t, int d, int64_t vstart,
+                      int64_t vrows, hipStream_t st) {
+    if (t == 0) return;
+    hipLaunchKernelGGL(embedding_kernel, dim3(t), dim3(256), 0, st, ids, table, out, d, vstart, vrows);
+}
+
+void launch_rmsnorm(const uint16_t* x, uint16_t* resid, const uint16_t* w, uint16_t* y, int rows, int d, float eps,
+                    hipStream_t st) {
+    if (rows == 0) return;
+    const int nv = d / 8;
+    const dim3 g(rows), b(256);
+#define RMS_CASE(V)                                                                                         \
+    if (nv <= 256 * V) {                                                                                    \
+        if (resid) hipLaunchKernelGGL((rmsnorm_kernel<V, true>), g, b, 0, st, x, resid, w, y, d, eps);       \
+        else hipLaunchKernelGGL((rmsnorm_kernel<V, false>), g, b, 0, st, x, resid, w, y, d, eps);           \
+        return;                                                                                             \
+    }
+    RMS_CASE(1) RMS_CASE(2) RMS_CASE(4) RMS_CASE(8)
+#undef RMS_CASE
+}
+
+void launch_rope_kv_write(const uint16_t* qkv, const int32_t* pos, const int32_t* tok_seq, const int32_t* block_table,
+                          int bt_stride, const float* cos_sin, uint16_t* q_out, uint16_t* k_cache, uint16_t* v_cache,
+                          int t, int hq, int hkv, int block_size, int write_q, hipStream_t st) {
+    if (t == 0) return;
+    const int nh = hq + 2 * hkv;
+    hipLaunchKernelGGL(rope_kv_write_kernel, dim3(t, (nh + 31) / 32), dim3(256), 0, st, qkv, pos, tok_seq,
+                       block_table, bt_stride, cos_sin, q_out, k_cache, v_cache, hq, hkv, block_size, write_q);
+}
+
+void launch_silu_mul(const uint16_t* gu, uint16_t* out, int64_t rows, int f, hipStream_t st) {
+    if (rows == 0) return;
+    const int64_t total = rows * (f / 8);
+    int64_t blocks = (total + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(silu_mul_kernel, dim3((unsigned)blocks), dim3(256), 0, st, gu, out, rows, f);
+}
+
+}  // namespace chronos

@@ -1,1 +1,100 @@
+"""Constrained decoding: grammar registry + device-resident token automaton (SURVEY.md §2.1 X6, §7.3 hard part 2).
 
+All grammars live in ONE global state space so a decode batch can mix requests with different ``format`` values
+(``"json"``, a JSON schema, or none) in a single sampler launch:
+
+* global state 0 is DONE (every grammar's accepting path ends there through an EOS token);
+* each grammar appends its states; a request starts in its grammar's start state;
+* the device table ``next[cap, V]`` (int16) and ``dist[cap]`` are preallocated at a fixed capacity, so graphs captured
+  against them stay valid when a new schema is registered at run time.
+"""
+from __future__ import annotations
+
+import threading
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import grammar as G
+
+DONE = 0
+
+
+@dataclass
+class CompiledGrammar:
+    key: str
+    start: int          # global start state
+    num_states: int
+    dfa: G.ByteDFA | None
+
+
+class GrammarBank:
+    def __init__(self, token_bytes: list[bytes], stop_ids: tuple[int, ...], vocab: int, capacity: int = 2048,
+                 device="cpu", max_string: int = 160, json_depth: int = 3, max_ws: int = 1):
+        self.token_bytes = token_bytes
+        self.stop_ids = tuple(stop_ids)
+        self.vocab = vocab
+        self.capacity = capacity
+        self.device = torch.device(device)
+        self.max_string, self.json_depth, self.max_ws = max_string, json_depth, max_ws
+        self.next = torch.full((capacity, vocab), -1, dtype=torch.int16, device=self.device)
+        self.dist = torch.full((capacity,), 32767, dtype=torch.int16, device=self.device)
+        self.dist[DONE] = 0
+        self.used = 1
+        self._host_dist: list[int] = [0]
+        self._by_key: dict[str, CompiledGrammar] = {}
+        self._lock = threading.Lock()
+        self._free_start = self._add_free()
+
+    # ---- registration -------------------------------------------------------------------------------------------
+    def _append(self, nxt: np.ndarray, dist: np.ndarray) -> int:
+        """nxt/dist use local ids with the local DONE = last row; returns the global id of local state 0."""
+        n = nxt.shape[0] - 1  # drop the local DONE row
+        if self.used + n > self.capacity:
+            raise RuntimeError(f"grammar bank full ({self.used}+{n} > {self.capacity} states)")
+        base = self.used
+        local_done = n
+        g = nxt[:n].astype(np.int32)
+        g = np.where(g < 0, -1, np.where(g == local_done, DONE, g + base)).astype(np.int16)
+        self.next[base:base + n] = torch.from_numpy(g).to(self.device)
+        self.dist[base:base + n] = torch.from_numpy(dist[:n].astype(np.int16)).to(self.device)
+        self._host_dist += [int(x) for x in dist[:n]]
+        self.used += n
+        return base
+
+    def _add_free(self) -> int:
+        """Unconstrained text: one state, every non-special token loops, a stop token ends."""
+        row = np.array([0 if b else -1 for b in self.token_bytes[: self.vocab]] + [-1] * max(0, self.vocab - len(self.token_bytes)),
+                       dtype=np.int16)
+        for s in self.stop_ids:
+            if s < self.vocab:
+                row[s] = 1
+        nxt = np.stack([row, np.full(self.vocab, -1, np.int16)])
+        dist = np.array([1, 0], dtype=np.int16)
+        cg = CompiledGrammar("null", self._append(nxt, dist), 1, None)
+        self._by_key["null"] = cg
+        return cg.start
+
+    def get(self, fmt) -> CompiledGrammar:
+        key = G.format_key(fmt if fmt not in ("", False) else None)
+        with self._lock:
+            if key in self._by_key:
+                return self._by_key[key]
+            node = G.grammar_for_format(fmt, self.json_depth, self.max_ws, self.max_string)
+            dfa = G.compile_dfa(node)
+            from ...native import constrain_lib
+
+            lib = constrain_lib()
+            toks = list(self.token_bytes[: self.vocab]) + [b""] * max(0, self.vocab - len(self.token_bytes))
+            nxt, dist, _live = lib.compile_token_dfa(dfa.trans, dfa.accept, toks, list(self.stop_ids), dfa.start)
+            cg = CompiledGrammar(key, self._append(np.asarray(nxt), np.asarray(dist)), dfa.num_states, dfa)
+            self._by_key[key] = cg
+            return cg
+
+    # ---- host-side helpers (tests, CPU engine) -----------------------------------------------------------------
+    def step(self, state: int, tok: int) -> int:
+        return int(self.next[state, tok])
+
+    def min_tokens(self, state: int) -> int:
+        return self._host_dist[state]

@@ -1,0 +1,381 @@
+"""The Brain's serving engine: continuous batching over paged KV with graph-captured, grammar-constrained decode.
+
+Replaces what Ollama + llama.cpp did for the reference:
+
+* **admission**: a request gets a decode *slot* and ALL the KV blocks it can ever need (prompt + num_predict) up
+  front, so a running sequence never stalls or gets preempted mid-verdict; KV is sized from the HBM budget
+  (288 GB per MI355X — 1-2 M tokens for 8B);
+* **prefill**: waiting prompts are packed into one flattened token stream (chunked to ``max_prefill_tokens``, so a
+  128k-token chain context prefills in pieces that attend to the paged prefix);
+* **decode**: all slots advance together; the step (32 layers + LM head + the constrained sampler, which also
+  advances ids/positions/context/DFA state on device) is captured once per power-of-two slot bucket into a hipGraph
+  holding ``decode_burst`` unrolled steps, so one host call runs e.g. 8 verdict tokens for every live stream;
+* **harvest**: after each step the host reads the slot states once, detokenizes finished verdicts and frees slots.
+
+The reference's ``analyze_sequence`` blocked the sensor for one chain at a time (quirk Q1); here thousands of chains
+are in flight and each returns as soon as its own verdict closes.
+"""
+from __future__ import annotations
+
+import collections
+import itertools
+import logging
+import math
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Any, Callable, Optional
+
+import torch
+
+from ... import ops
+from ...models.llama import KVCache, LlamaModel, StepBatch, build_model, make_prefill_batch
+from ...parallel.tp import TPContext
+from ..constrain import DONE, GrammarBank
+from ..tokenizer import load_tokenizer
+from .block_manager import BlockManager
+
+log = logging.getLogger("chronos.engine")
+
+
+@dataclass
+class EngineConfig:
+    model: str = "llama3-8b"
+    checkpoint: Optional[str] = None
+    tokenizer: Optional[str] = None
+    device: str = "cuda"
+    seed: int = 0
+    max_slots: int = 256           # concurrent sequences in the decode batch
+    block_size: int = 16
+    max_model_len: int = 4096      # prompt + generated tokens per sequence
+    kv_blocks: int = 0             # 0 = size from HBM (kv_fraction of free memory, capped at what max_slots can use)
+    kv_fraction: float = 0.9
+    reserve_gb: float = 12.0       # activations / graph pools / grammar table headroom
+    max_prefill_tokens: int = 16384
+    default_num_predict: int = 128
+    max_out: int = 512             # hard cap on generated tokens per request
+    decode_burst: int = 8
+    use_graphs: bool = True
+    grammar_capacity: int = 2048
+    max_string: int = 160          # default maxLength for schema strings without one (keeps verdicts short)
+    prefill_nqt: int = 2
+
+
+@dataclass
+class Request:
+    rid: int
+    prompt_ids: list
+    fmt: Any = None
+    num_predict: int = 128
+    temperature: float = 0.0
+    seed: int = 0
+    callback: Optional[Callable[["Request"], None]] = None
+    meta: dict = field(default_factory=dict)
+    # runtime
+    slot: int = -1
+    blocks: list = field(default_factory=list)
+    prefilled: int = 0
+    start_state: int = 0
+    out_ids: list = field(default_factory=list)
+    text: str = ""
+    done_reason: str = ""
+    error: Optional[str] = None
+    t_submit: float = 0.0
+    t_admit: float = 0.0
+    t_first: float = 0.0
+    t_done: float = 0.0
+
+    @property
+    def latency(self) -> float:
+        return self.t_done - self.t_submit
+
+
+def _bucket(n: int) -> int:
+    return 1 << max(0, (n - 1).bit_length())
+
+
+class Engine:
+    def __init__(self, cfg: EngineConfig, tp: TPContext | None = None, model: LlamaModel | None = None,
+                 tokenizer=None):
+        self.cfg = cfg
+        self.tp = tp or TPContext.single()
+        self.device = torch.device(cfg.device)
+        if self.device.type == "cuda":
+            torch.cuda.set_device(self.device)
+            ops.load()  # the HIP library must load on a GPU engine — never a silent eager fallback
+        self.tok = tokenizer or load_tokenizer(cfg.tokenizer)
+        t0 = time.perf_counter()
+        self.model = model or build_model(cfg.model, self.device, self.tp, cfg.seed, cfg.checkpoint,
+                                          max_position=cfg.max_model_len + 16)
+        self.load_seconds = time.perf_counter() - t0
+        mc = self.model.cfg
+        self.bank = GrammarBank(self.tok.token_bytes_list(), self.tok.stop_ids, mc.vocab_size, cfg.grammar_capacity,
+                                self.device, max_string=cfg.max_string)
+        # ---- KV sizing ----
+        bs = cfg.block_size
+        self.max_blocks_per_seq = (cfg.max_model_len + bs - 1) // bs
+        need = cfg.max_slots * self.max_blocks_per_seq + 1
+        nb = cfg.kv_blocks
+        if nb <= 0:
+            if self.device.type == "cuda":
+                free, _ = torch.cuda.mem_get_info(self.device)
+                budget = max(0.0, free * cfg.kv_fraction - cfg.reserve_gb * 2**30)
+                nb = int(budget // KVCache.bytes_per_block(mc, self.tp, bs))
+                nb = max(2, min(nb, need))
+            else:
+                nb = need
+        self.kv = KVCache(mc, self.tp, nb, bs, self.device)
+        self.blocks = BlockManager(nb, bs)
+        # ---- slot state (device) ----
+        S, dev = cfg.max_slots, self.device
+        i32 = dict(dtype=torch.int32, device=dev)
+        self.s_ids = torch.zeros(S, **i32)
+        self.s_pos = torch.zeros(S, **i32)
+        self.s_ctx = torch.ones(S, **i32)
+        self.s_state = torch.full((S,), -1, **i32)
+        self.s_rem = torch.zeros(S, **i32)
+        self.s_nout = torch.zeros(S, **i32)
+        self.s_seed = torch.zeros(S, **i32)
+        self.s_temp = torch.zeros(S, dtype=torch.float32, device=dev)
+        self.s_out = torch.zeros(S, cfg.max_out, **i32)
+        self.s_bt = torch.zeros(S, self.max_blocks_per_seq, **i32)
+        self.s_row = torch.full((S,), -1, **i32)
+        self.ar = torch.arange(S + 1, **i32)
+        self.ar64 = torch.arange(S, dtype=torch.int64, device=dev)
+        # ---- scheduling state ----
+        self.waiting: collections.deque[Request] = collections.deque()
+        self.prefilling: list[Request] = []
+        self.running: dict[int, Request] = {}
+        self.free_slots = list(range(S - 1, -1, -1))
+        self._rid = itertools.count()
+        self._graphs: dict[int, torch.cuda.CUDAGraph] = {}
+        self._graph_pool = None
+        self.stats = collections.Counter()
+        self._lock = threading.Lock()
+        if self.device.type == "cuda":
+            self._warmup()
+
+    # ------------------------------------------------------------------------------------------------------------
+    # public API
+    # ------------------------------------------------------------------------------------------------------------
+    def submit(self, prompt: str | list, fmt=None, num_predict: int | None = None, temperature: float = 0.0,
+               seed: int = 0, raw: bool = False, system: str | None = None,
+               callback: Callable[[Request], None] | None = None, meta: dict | None = None) -> Request:
+        ids = prompt if isinstance(prompt, list) else self.tok.chat_ids(prompt, system=system, raw=raw)
+        n = num_predict if num_predict and num_predict > 0 else self.cfg.default_num_predict
+        n = min(n, self.cfg.max_out, self.cfg.max_model_len - len(ids))
+        req = Request(next(self._rid), ids, fmt, n, float(temperature or 0.0), int(seed or 0), callback, meta or {})
+        req.t_submit = time.perf_counter()
+        if n <= 0:
+            req.error = f"prompt of {len(ids)} tokens exceeds max_model_len {self.cfg.max_model_len}"
+            self._finish(req, "error")
+            return req
+        try:
+            req.start_state = self.bank.get(fmt).start
+        except Exception as e:  # bad schema: report, never crash the engine
+            req.error = f"invalid format: {e}"
+            self._finish(req, "error")
+            return req
+        with self._lock:
+            self.waiting.append(req)
+        return req
+
+    def has_work(self) -> bool:
+        return bool(self.waiting or self.prefilling or self.running)
+
+    def step(self) -> list[Request]:
+        """One scheduling iteration: admit + prefill if anything is waiting, else one decode burst."""
+        self._admit()
+        if self.prefilling:
+            self._prefill_step()
+        elif self.running:
+            self._decode_burst()
+        return self._harvest()
+
+    def run_until_idle(self, max_steps: int = 10**9) -> list[Request]:
+        done = []
+        for _ in range(max_steps):
+            if not self.has_work():
+                break
+            done += self.step()
+        return done
+
+    def generate(self, prompts: list, fmt=None, num_predict: int | None = None, temperature: float = 0.0) -> list[Request]:
+        reqs = [self.submit(p, fmt, num_predict, temperature) for p in prompts]
+        self.run_until_idle()
+        return reqs
+
+    # ------------------------------------------------------------------------------------------------------------
+    # scheduling
+    # ------------------------------------------------------------------------------------------------------------
+    def _admit(self) -> None:
+        with self._lock:
+            while self.waiting and self.free_slots:
+                req = self.waiting[0]
+                nblk = self.blocks.blocks_for(len(req.prompt_ids) + req.num_predict)
+                if not self.blocks.can_alloc(nblk):
+                    break
+                self.waiting.popleft()
+                req.blocks = self.blocks.alloc(nblk)
+                req.slot = self.free_slots.pop()
+                req.t_admit = time.perf_counter()
+                self.prefilling.append(req)
+                row = torch.zeros(self.max_blocks_per_seq, dtype=torch.int32)
+                row[:nblk] = torch.tensor(req.blocks, dtype=torch.int32)
+                self.s_bt[req.slot].copy_(row, non_blocking=True)
+
+    def _prefill_step(self) -> None:
+        budget = self.cfg.max_prefill_tokens
+        chunks, starts, bts, reqs = [], [], [], []
+        for req in self.prefilling:
+            if budget <= 0:
+                break
+            n = min(len(req.prompt_ids) - req.prefilled, budget)
+            chunks.append(req.prompt_ids[req.prefilled:req.prefilled + n])
+            starts.append(req.prefilled)
+            bts.append(req.blocks)
+            reqs.append(req)
+            budget -= n
+        sb = make_prefill_batch(chunks, starts, bts, self.model.cfg, self.tp, self.device,
+                                max_blocks=self.max_blocks_per_seq, nqt=self.cfg.prefill_nqt)
+        logits = self.model.forward(sb, self.kv)
+        done_rows, done_reqs = [], []
+        for i, (req, ch) in enumerate(zip(reqs, chunks)):
+            req.prefilled += len(ch)
+            if req.prefilled == len(req.prompt_ids):
+                done_rows.append(i)
+                done_reqs.append(req)
+        self.stats["prefill_tokens"] += int(sb.ids.numel())
+        self.stats["prefill_steps"] += 1
+        if not done_reqs:
+            return
+        # initialise the finished prompts' slots and sample their first token
+        slots = torch.tensor([r.slot for r in done_reqs], dtype=torch.int64)
+        plen = torch.tensor([len(r.prompt_ids) for r in done_reqs], dtype=torch.int32)
+        dv = lambda t: t.to(self.device, non_blocking=True)  # noqa: E731
+        sl = dv(slots)
+        self.s_state[sl] = dv(torch.tensor([r.start_state for r in done_reqs], dtype=torch.int32))
+        self.s_rem[sl] = dv(torch.tensor([r.num_predict for r in done_reqs], dtype=torch.int32))
+        self.s_pos[sl] = dv(plen - 1)
+        self.s_ctx[sl] = dv(plen)
+        self.s_nout[sl] = 0
+        self.s_temp[sl] = dv(torch.tensor([r.temperature for r in done_reqs], dtype=torch.float32))
+        self.s_seed[sl] = dv(torch.tensor([r.seed for r in done_reqs], dtype=torch.int32))
+        self.s_row.fill_(-1)
+        self.s_row[sl] = dv(torch.tensor(done_rows, dtype=torch.int32))
+        ops.constrained_sample(logits, self.s_row, self.bank.next, self.bank.dist, DONE, self.s_state, self.s_rem,
+                               self.s_temp, self.s_seed, self.s_ids, self.s_pos, self.s_ctx, self.s_nout, self.s_out)
+        now = time.perf_counter()
+        for r in done_reqs:
+            r.t_first = now
+            self.prefilling.remove(r)
+            self.running[r.slot] = r
+
+    def _decode_rows(self) -> int:
+        return _bucket(max(self.running) + 1) if self.running else 0
+
+    def _decode_once(self, n: int, nsplit: int) -> None:
+        sb = StepBatch(self.s_ids[:n], self.s_pos[:n], self.ar[:n], self.s_bt[:n], self.ar[:n + 1], self.s_ctx[:n],
+                       self.ar64[:n], None, n, 1, nsplit)
+        logits = self.model.forward(sb, self.kv)
+        ops.constrained_sample(logits, None, self.bank.next, self.bank.dist, DONE, self.s_state[:n], self.s_rem[:n],
+                               self.s_temp[:n], self.s_seed[:n], self.s_ids[:n], self.s_pos[:n], self.s_ctx[:n],
+                               self.s_nout[:n], self.s_out[:n])
+
+    def _nsplit(self, n: int) -> int:
+        return ops.pick_nsplit(n * self.model.hkv, self.cfg.max_model_len)
+
+    def _decode_burst(self) -> None:
+        n = min(self._decode_rows(), self.cfg.max_slots)
+        k = self.cfg.decode_burst
+        if self.device.type == "cuda" and self.cfg.use_graphs:
+            g = self._graphs.get(n)
+            if g is None:
+                g = self._capture(n)
+            g.replay()
+        else:
+            for _ in range(k):
+                self._decode_once(n, self._nsplit(n))
+        self.stats["decode_steps"] += k
+        self.stats["decode_row_steps"] += k * n
+
+    def _capture(self, n: int) -> "torch.cuda.CUDAGraph":
+        if self._graph_pool is None:
+            self._graph_pool = torch.cuda.graph_pool_handle()
+        g = torch.cuda.CUDAGraph()
+        ns = self._nsplit(n)
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, pool=self._graph_pool):
+            for _ in range(self.cfg.decode_burst):
+                self._decode_once(n, ns)
+        self._graphs[n] = g
+        self.stats["graphs_captured"] += 1
+        return g
+
+    def _warmup(self) -> None:
+        """Initialise library handles / kernels with every slot empty (scratch block only), so graph capture later
+        never has to run a lazily-initialising op."""
+        n = self.cfg.max_slots
+        self._decode_once(n, self._nsplit(n))
+        torch.cuda.synchronize()
+
+    def _harvest(self) -> list[Request]:
+        if not self.running:
+            return []
+        n = self._decode_rows()
+        st = self.s_state[:n].cpu()
+        finished = [r for s, r in self.running.items() if int(st[s]) == DONE]
+        if not finished:
+            return []
+        nout = self.s_nout[:n].cpu()
+        outs = self.s_out[:n].cpu()
+        now = time.perf_counter()
+        reset = []
+        for r in finished:
+            k = int(nout[r.slot])
+            ids = outs[r.slot, :min(k, self.cfg.max_out)].tolist()
+            stop = bool(ids) and ids[-1] in self.tok.stop_ids
+            r.out_ids = ids[:-1] if stop else ids
+            r.text = self.tok.decode(r.out_ids)
+            r.t_done = now
+            del self.running[r.slot]
+            self.blocks.release(r.blocks)
+            reset.append(r.slot)
+            self.free_slots.append(r.slot)
+            self._finish(r, "stop" if stop else "length", timed=False)
+        self.free_slots.sort(reverse=True)  # lowest slot first keeps the decode bucket small
+        idx = torch.tensor(reset, dtype=torch.int64).to(self.device)
+        self.s_state[idx] = -1
+        self.s_bt[idx] = 0
+        self.s_pos[idx] = 0
+        self.s_ctx[idx] = 1
+        self.stats["completed"] += len(finished)
+        self.stats["generated_tokens"] += sum(len(r.out_ids) for r in finished)
+        return finished
+
+    def _finish(self, req: Request, reason: str, timed: bool = True) -> None:
+        req.done_reason = reason
+        if timed or not req.t_done:
+            req.t_done = time.perf_counter()
+        if req.callback is not None:
+            try:
+                req.callback(req)
+            except Exception:  # a client callback must never take the engine down
+                log.exception("request callback failed")
+
+    def result_json(self, req: Request, model_name: str = "llama3") -> dict:
+        """Ollama /api/generate (stream=false) response body."""
+        ns = lambda s: int(max(0.0, s) * 1e9)  # noqa: E731
+        return {
+            "model": model_name,
+            "created_at": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime()),
+            "response": req.text,
+            "done": True,
+            "done_reason": req.done_reason,
+            "total_duration": ns(req.t_done - req.t_submit),
+            "load_duration": 0,
+            "prompt_eval_count": len(req.prompt_ids),
+            "prompt_eval_duration": ns((req.t_first or req.t_done) - (req.t_admit or req.t_submit)),
+            "eval_count": len(req.out_ids),
+            "eval_duration": ns(req.t_done - (req.t_first or req.t_done)),
+        }

@@ -1,0 +1,486 @@
+"""Llama-3 / 3.1 for the Brain: config presets, TP-sharded weights, random init,
+HF-safetensors and Meta ``consolidated.*.pth`` loaders, and the varlen paged-KV forward.
+
+The reference never holds a model: it POSTs to Ollama's ``llama3`` (chronos_sensor.py:10,118; README.md:21).  This is
+the model Ollama served, re-built MI355X-first:
+
+* weights in the layout the kernels want: fused ``wqkv`` [(Hq+2Hkv)*128, d] and ``w_gu`` [2F, d] (one GEMM each),
+  bf16, resident for the life of the engine (no lazy load: reference quirk X8 / screenshot chain 1);
+* one flattened token stream per step (prefill chunks and decode tokens alike) with per-sequence metadata, so
+  continuous batching never pads;
+* every non-GEMM op is a gfx950 HIP kernel (chronos.ops); TP collectives sit exactly after the row-parallel GEMMs
+  (o_proj, down_proj), the vocab-parallel embedding and the LM head.
+"""
+from __future__ import annotations
+
+import glob
+import json
+import math
+import os
+from dataclasses import asdict, dataclass, field, replace
+from typing import Optional
+
+import torch
+
+from .. import ops
+from ..parallel.tp import TPContext
+
+
+@dataclass
+class LlamaConfig:
+    name: str = "llama3-8b"
+    vocab_size: int = 128256
+    hidden_size: int = 4096
+    intermediate_size: int = 14336
+    num_layers: int = 32
+    num_heads: int = 32
+    num_kv_heads: int = 8
+    head_dim: int = 128
+    rms_eps: float = 1e-5
+    rope_theta: float = 500000.0
+    rope_scaling: Optional[dict] = None
+    max_position: int = 8192
+    tie_word_embeddings: bool = False
+    init_std: float = 0.02
+
+    @property
+    def group(self) -> int:
+        return self.num_heads // self.num_kv_heads
+
+    def param_count(self) -> int:
+        d, f, v = self.hidden_size, self.intermediate_size, self.vocab_size
+        qkv = d * (self.num_heads + 2 * self.num_kv_heads) * self.head_dim
+        per = qkv + self.num_heads * self.head_dim * d + 3 * d * f + 2 * d
+        return self.num_layers * per + v * d * (1 if self.tie_word_embeddings else 2) + d
+
+    @classmethod
+    def from_hf(cls, cfg: dict, name: str = "hf") -> "LlamaConfig":
+        return cls(
+            name=name,
+            vocab_size=cfg["vocab_size"],
+            hidden_size=cfg["hidden_size"],
+            intermediate_size=cfg["intermediate_size"],
+            num_layers=cfg["num_hidden_layers"],
+            num_heads=cfg["num_attention_heads"],
+            num_kv_heads=cfg.get("num_key_value_heads", cfg["num_attention_heads"]),
+            head_dim=cfg.get("head_dim", cfg["hidden_size"] // cfg["num_attention_heads"]),
+            rms_eps=cfg.get("rms_norm_eps", 1e-5),
+            rope_theta=cfg.get("rope_theta", 10000.0),
+            rope_scaling=cfg.get("rope_scaling"),
+            max_position=cfg.get("max_position_embeddings", 8192),
+            tie_word_embeddings=cfg.get("tie_word_embeddings", False),
+        )
+
+    @classmethod
+    def from_meta(cls, params: dict, name: str = "meta") -> "LlamaConfig":
+        d = params["dim"]
+        nh = params["n_heads"]
+        mult = params.get("ffn_dim_multiplier", 1.0)
+        hidden = int(2 * (4 * d) / 3)
+        hidden = int(mult * hidden)
+        mo = params.get("multiple_of", 256)
+        hidden = mo * ((hidden + mo - 1) // mo)
+        scaling = None
+        if params.get("use_scaled_rope"):
+            scaling = dict(rope_type="llama3", factor=8.0, low_freq_factor=1.0, high_freq_factor=4.0,
+                           original_max_position_embeddings=8192)
+        return cls(name=name, vocab_size=params.get("vocab_size", 128256), hidden_size=d, intermediate_size=hidden,
+                   num_layers=params["n_layers"], num_heads=nh, num_kv_heads=params.get("n_kv_heads", nh),
+                   head_dim=d // nh, rms_eps=params.get("norm_eps", 1e-5), rope_theta=params.get("rope_theta", 500000.0),
+                   rope_scaling=scaling, max_position=131072 if scaling else 8192)
+
+
+_LLAMA31_SCALING = dict(rope_type="llama3", factor=8.0, low_freq_factor=1.0, high_freq_factor=4.0,
+                        original_max_position_embeddings=8192)
+
+PRESETS: dict[str, LlamaConfig] = {
+    "llama3-8b": LlamaConfig(),
+    "llama3-70b": LlamaConfig(name="llama3-70b", hidden_size=8192, intermediate_size=28672, num_layers=80,
+                              num_heads=64, num_kv_heads=8),
+    "llama3.1-8b": LlamaConfig(name="llama3.1-8b", rope_scaling=_LLAMA31_SCALING, max_position=131072),
+    "llama3.1-70b": LlamaConfig(name="llama3.1-70b", hidden_size=8192, intermediate_size=28672, num_layers=80,
+                                num_heads=64, num_kv_heads=8, rope_scaling=_LLAMA31_SCALING, max_position=131072),
+    # test-sized models with the real vocabulary and head_dim (the kernels assume head_dim 128)
+    "tiny": LlamaConfig(name="tiny", hidden_size=256, intermediate_size=512, num_layers=2, num_heads=4,
+                        num_kv_heads=2, max_position=4096),
+    "small": LlamaConfig(name="small", hidden_size=1024, intermediate_size=2816, num_layers=4, num_heads=8,
+                         num_kv_heads=2, max_position=8192),
+}
+
+
+def get_config(name: str) -> LlamaConfig:
+    if name not in PRESETS:
+        raise KeyError(f"unknown model preset {name!r}; have {sorted(PRESETS)}")
+    return replace(PRESETS[name])
+
+
+# -----------------------------------------------------------------------------------------------------------------
+# RoPE tables
+# -----------------------------------------------------------------------------------------------------------------
+
+
+def rope_inv_freq(cfg: LlamaConfig) -> torch.Tensor:
+    d = cfg.head_dim
+    inv = 1.0 / (cfg.rope_theta ** (torch.arange(0, d, 2, dtype=torch.float64) / d))
+    sc = cfg.rope_scaling
+    if sc and sc.get("rope_type", sc.get("type")) == "llama3":
+        factor = sc["factor"]
+        lo, hi = sc["low_freq_factor"], sc["high_freq_factor"]
+        old = sc["original_max_position_embeddings"]
+        lo_wl, hi_wl = old / lo, old / hi
+        wl = 2 * math.pi / inv
+        inv_l = torch.where(wl > lo_wl, inv / factor, inv)
+        smooth = (old / wl - lo) / (hi - lo)
+        smoothed = (1 - smooth) * inv_l / factor + smooth * inv_l
+        medium = ~(wl < hi_wl) & ~(wl > lo_wl)
+        inv = torch.where(medium, smoothed, inv_l)
+    return inv
+
+
+def rope_table(cfg: LlamaConfig, max_pos: int, device=None) -> torch.Tensor:
+    """cos_sin[p, 0:64] = cos(p * f), [64:128] = sin(p * f), f32 (consumed by the rope_kv_write kernel)."""
+    inv = rope_inv_freq(cfg)
+    p = torch.arange(max_pos, dtype=torch.float64)
+    fr = torch.outer(p, inv)
+    return torch.cat([fr.cos(), fr.sin()], dim=1).float().to(device)
+
+
+# -----------------------------------------------------------------------------------------------------------------
+# weights
+# -----------------------------------------------------------------------------------------------------------------
+
+
+@dataclass
+class LayerWeights:
+    attn_norm: torch.Tensor
+    wqkv: torch.Tensor
+    wo: torch.Tensor
+    mlp_norm: torch.Tensor
+    w_gu: torch.Tensor
+    w_down: torch.Tensor
+
+
+@dataclass
+class LlamaWeights:
+    embed: torch.Tensor            # [V_local, d] (vocab-parallel shard)
+    layers: list
+    norm: torch.Tensor
+    lm_head: torch.Tensor          # [V_local, d]
+    vocab_start: int = 0
+
+    def nbytes(self) -> int:
+        n = self.embed.numel() + self.norm.numel() + (0 if self.lm_head is self.embed else self.lm_head.numel())
+        for l in self.layers:
+            n += sum(t.numel() for t in (l.attn_norm, l.wqkv, l.wo, l.mlp_norm, l.w_gu, l.w_down))
+        return 2 * n
+
+
+def _shard_rows(t: torch.Tensor, rank: int, world: int) -> torch.Tensor:
+    n = t.shape[0] // world
+    return t[rank * n:(rank + 1) * n]
+
+
+def _shard_cols(t: torch.Tensor, rank: int, world: int) -> torch.Tensor:
+    n = t.shape[1] // world
+    return t[:, rank * n:(rank + 1) * n]
+
+
+def _local_heads(cfg: LlamaConfig, tp: TPContext) -> tuple[int, int]:
+    if cfg.num_heads % tp.world or cfg.num_kv_heads % tp.world:
+        raise ValueError(f"TP={tp.world} must divide q heads {cfg.num_heads} and kv heads {cfg.num_kv_heads}")
+    return cfg.num_heads // tp.world, cfg.num_kv_heads // tp.world
+
+
+def assemble_layer(cfg: LlamaConfig, tp: TPContext, full: dict, device, dtype=torch.bfloat16) -> LayerWeights:
+    """Full (unsharded) HF-named tensors of one layer -> this rank's fused shard."""
+    r, w = tp.rank, tp.world
+    D = cfg.head_dim
+    q = full["q"].view(cfg.num_heads, D, -1)
+    k = full["k"].view(cfg.num_kv_heads, D, -1)
+    v = full["v"].view(cfg.num_kv_heads, D, -1)
+    hq, hkv = _local_heads(cfg, tp)
+    qs = q[r * hq:(r + 1) * hq].reshape(hq * D, -1)
+    ks = k[r * hkv:(r + 1) * hkv].reshape(hkv * D, -1)
+    vs = v[r * hkv:(r + 1) * hkv].reshape(hkv * D, -1)
+    wqkv = torch.cat([qs, ks, vs], 0)
+    wo = _shard_cols(full["o"], r, w)
+    w_gu = torch.cat([_shard_rows(full["gate"], r, w), _shard_rows(full["up"], r, w)], 0)
+    w_down = _shard_cols(full["down"], r, w)
+    cv = lambda t: t.to(device=device, dtype=dtype).contiguous()  # noqa: E731
+    return LayerWeights(cv(full["attn_norm"]), cv(wqkv), cv(wo), cv(full["mlp_norm"]), cv(w_gu), cv(w_down))
+
+
+def random_weights(cfg: LlamaConfig, tp: TPContext | None = None, device="cpu", seed: int = 0,
+                   dtype=torch.bfloat16) -> LlamaWeights:
+    """Random-init weights with the real architecture (the benchmark's model; no checkpoints offline).
+
+    Every rank draws the FULL tensor from the same seeded generator and keeps its shard, so a TP run is numerically
+    the same model as TP=1.  Generation happens on ``device`` (GPU: ~1 s for 8B).
+    """
+    tp = tp or TPContext.single()
+    dev = torch.device(device)
+    gen = torch.Generator(device=dev)
+    d, f, D = cfg.hidden_size, cfg.intermediate_size, cfg.head_dim
+    std = cfg.init_std
+
+    def rnd(*shape):
+        t = torch.empty(*shape, device=dev, dtype=dtype)
+        t.normal_(0.0, std, generator=gen)
+        return t
+
+    def ones(n):
+        return torch.ones(n, device=dev, dtype=dtype)
+
+    gen.manual_seed(seed)
+    embed_full = rnd(cfg.vocab_size, d)
+    vs = cfg.vocab_size // tp.world
+    embed = embed_full[tp.rank * vs:(tp.rank + 1) * vs].contiguous()
+    del embed_full
+    layers = []
+    for i in range(cfg.num_layers):
+        gen.manual_seed(seed * 1000003 + i + 1)
+        full = dict(
+            attn_norm=ones(d),
+            q=rnd(cfg.num_heads * D, d), k=rnd(cfg.num_kv_heads * D, d), v=rnd(cfg.num_kv_heads * D, d),
+            o=rnd(d, cfg.num_heads * D), mlp_norm=ones(d),
+            gate=rnd(f, d), up=rnd(f, d), down=rnd(d, f),
+        )
+        layers.append(assemble_layer(cfg, tp, full, dev, dtype))
+        del full
+    gen.manual_seed(seed * 1000003 + 999983)
+    if cfg.tie_word_embeddings:
+        lm_head = embed
+    else:
+        lm_full = rnd(cfg.vocab_size, d)
+        lm_head = lm_full[tp.rank * vs:(tp.rank + 1) * vs].contiguous()
+        del lm_full
+    return LlamaWeights(embed, layers, ones(d), lm_head, vocab_start=tp.rank * vs)
+
+
+# ---- checkpoint loaders ----------------------------------------------------------------------------------------
+
+
+def _meta_permute(w: torch.Tensor, n_heads: int) -> torch.Tensor:
+    """Meta's interleaved-pair rotary layout -> HF rotate-half layout (the transform convert_llama_weights applies)."""
+    d1, d2 = w.shape
+    return w.view(n_heads, d1 // n_heads // 2, 2, d2).transpose(1, 2).reshape(d1, d2)
+
+
+def load_hf(path: str, tp: TPContext | None = None, device="cpu", dtype=torch.bfloat16) -> tuple[LlamaConfig, LlamaWeights]:
+    """HF layout: config.json + model*.safetensors (tensor names: SURVEY.md App. B)."""
+    from safetensors import safe_open
+
+    tp = tp or TPContext.single()
+    with open(os.path.join(path, "config.json")) as fh:
+        cfg = LlamaConfig.from_hf(json.load(fh), name=os.path.basename(path.rstrip("/")))
+    files = sorted(glob.glob(os.path.join(path, "*.safetensors")))
+    if not files:
+        raise FileNotFoundError(f"no *.safetensors in {path}")
+    index: dict[str, str] = {}
+    for fpath in files:
+        with safe_open(fpath, framework="pt") as f:
+            for k in f.keys():
+                index[k] = fpath
+    handles: dict[str, object] = {}
+
+    def get(name):
+        fp = index[name]
+        if fp not in handles:
+            handles[fp] = safe_open(fp, framework="pt")
+        return handles[fp].get_tensor(name)
+
+    vs = cfg.vocab_size // tp.world
+    embed = get("model.embed_tokens.weight")[tp.rank * vs:(tp.rank + 1) * vs].to(device=device, dtype=dtype).contiguous()
+    layers = []
+    for i in range(cfg.num_layers):
+        p = f"model.layers.{i}."
+        full = dict(
+            attn_norm=get(p + "input_layernorm.weight"), mlp_norm=get(p + "post_attention_layernorm.weight"),
+            q=get(p + "self_attn.q_proj.weight"), k=get(p + "self_attn.k_proj.weight"),
+            v=get(p + "self_attn.v_proj.weight"), o=get(p + "self_attn.o_proj.weight"),
+            gate=get(p + "mlp.gate_proj.weight"), up=get(p + "mlp.up_proj.weight"), down=get(p + "mlp.down_proj.weight"),
+        )
+        layers.append(assemble_layer(cfg, tp, full, device, dtype))
+    norm = get("model.norm.weight").to(device=device, dtype=dtype)
+    if cfg.tie_word_embeddings or "lm_head.weight" not in index:
+        lm_head = embed
+    else:
+        lm_head = get("lm_head.weight")[tp.rank * vs:(tp.rank + 1) * vs].to(device=device, dtype=dtype).contiguous()
+    return cfg, LlamaWeights(embed, layers, norm, lm_head, vocab_start=tp.rank * vs)
+
+
+def load_meta(path: str, tp: TPContext | None = None, device="cpu", dtype=torch.bfloat16) -> tuple[LlamaConfig, LlamaWeights]:
+    """Meta layout: params.json + consolidated.NN.pth (model-parallel shards are concatenated back first).
+    Loaded with ``weights_only=True`` (no pickled code is ever executed)."""
+    tp = tp or TPContext.single()
+    with open(os.path.join(path, "params.json")) as fh:
+        cfg = LlamaConfig.from_meta(json.load(fh), name=os.path.basename(path.rstrip("/")))
+    shards = [torch.load(f, map_location="cpu", weights_only=True, mmap=True)
+              for f in sorted(glob.glob(os.path.join(path, "consolidated.*.pth")))]
+    if not shards:
+        raise FileNotFoundError(f"no consolidated.*.pth in {path}")
+
+    def cat(name, dim):
+        ts = [s[name] for s in shards]
+        return ts[0] if len(ts) == 1 or ts[0].dim() == 1 else torch.cat(ts, dim)
+
+    vs = cfg.vocab_size // tp.world
+    embed = cat("tok_embeddings.weight", 1)[tp.rank * vs:(tp.rank + 1) * vs].to(device=device, dtype=dtype).contiguous()
+    layers = []
+    for i in range(cfg.num_layers):
+        p = f"layers.{i}."
+        full = dict(
+            attn_norm=cat(p + "attention_norm.weight", 0), mlp_norm=cat(p + "ffn_norm.weight", 0),
+            q=_meta_permute(cat(p + "attention.wq.weight", 0), cfg.num_heads),
+            k=_meta_permute(cat(p + "attention.wk.weight", 0), cfg.num_kv_heads),
+            v=cat(p + "attention.wv.weight", 0), o=cat(p + "attention.wo.weight", 1),
+            gate=cat(p + "feed_forward.w1.weight", 0), up=cat(p + "feed_forward.w3.weight", 0),
+            down=cat(p + "feed_forward.w2.weight", 1),
+        )
+        layers.append(assemble_layer(cfg, tp, full, device, dtype))
+    norm = cat("norm.weight", 0).to(device=device, dtype=dtype)
+    lm_head = cat("output.weight", 0)[tp.rank * vs:(tp.rank + 1) * vs].to(device=device, dtype=dtype).contiguous()
+    return cfg, LlamaWeights(embed, layers, norm, lm_head, vocab_start=tp.rank * vs)
+
+
+def load_checkpoint(path: str, tp: TPContext | None = None, device="cpu"):
+    if os.path.exists(os.path.join(path, "config.json")):
+        return load_hf(path, tp, device)
+    if os.path.exists(os.path.join(path, "params.json")):
+        return load_meta(path, tp, device)
+    raise FileNotFoundError(f"{path}: neither an HF (config.json) nor a Meta (params.json) Llama checkpoint")
+
+
+# -----------------------------------------------------------------------------------------------------------------
+# KV cache + step metadata
+# -----------------------------------------------------------------------------------------------------------------
+
+
+class KVCache:
+    """Paged KV: per layer K [NB, Hkv, BS, 128] (token rows) and V [NB, Hkv, 128, BS] (transposed, attention.hip).
+
+    One allocation for all layers, sized from the HBM budget (288 GB per MI355X).
+    """
+
+    def __init__(self, cfg: LlamaConfig, tp: TPContext, num_blocks: int, block_size: int = 16, device="cpu",
+                 dtype=torch.bfloat16):
+        _, hkv = _local_heads(cfg, tp)
+        self.num_blocks, self.block_size, self.hkv = num_blocks, block_size, hkv
+        per = hkv * block_size * cfg.head_dim
+        self.buf = torch.zeros(cfg.num_layers, 2, num_blocks, per, device=device, dtype=dtype)
+        self.k = [self.buf[l, 0].view(num_blocks, hkv, block_size, cfg.head_dim) for l in range(cfg.num_layers)]
+        self.v = [self.buf[l, 1].view(num_blocks, hkv, cfg.head_dim, block_size) for l in range(cfg.num_layers)]
+
+    @staticmethod
+    def bytes_per_block(cfg: LlamaConfig, tp: TPContext, block_size: int = 16) -> int:
+        _, hkv = _local_heads(cfg, tp)
+        return cfg.num_layers * 2 * hkv * block_size * cfg.head_dim * 2
+
+
+@dataclass
+class StepBatch:
+    """One forward step over a flattened token stream (any mix of prefill chunks and decode tokens)."""
+    ids: torch.Tensor          # [T] int32
+    pos: torch.Tensor          # [T] int32
+    tok_seq: torch.Tensor      # [T] int32  token -> row of block_table / ctx_len
+    block_table: torch.Tensor  # [B, max_blocks] int32
+    q_start: torch.Tensor      # [B+1] int32
+    ctx_len: torch.Tensor      # [B] int32 kv length after this step
+    last_idx: torch.Tensor     # [B] int64 token index whose logits are wanted
+    tiles: Optional[torch.Tensor]  # [ntiles, 2] int32, None = decode mode (one token per sequence, seq i = token i)
+    ntiles: int
+    nqt: int = 1
+    nsplit: int = 1
+
+
+def make_prefill_batch(prompts: list[list[int]], starts: list[int], block_tables: list[list[int]], cfg: LlamaConfig,
+                       tp: TPContext, device, max_blocks: int | None = None, nqt: int = 2,
+                       ctx_totals: list[int] | None = None) -> StepBatch:
+    """Host builder for a (chunked) prefill step.  prompts[b] are the tokens of this chunk, starts[b] the position of
+    its first token (prefix already in the cache)."""
+    hq, hkv = _local_heads(cfg, tp)
+    ids, pos, tok_seq, qs = [], [], [], [0]
+    for b, (toks, s0) in enumerate(zip(prompts, starts)):
+        ids += toks
+        pos += list(range(s0, s0 + len(toks)))
+        tok_seq += [b] * len(toks)
+        qs.append(qs[-1] + len(toks))
+    ctx = [s0 + len(t) for t, s0 in zip(prompts, starts)]
+    mb = max_blocks or max(len(x) for x in block_tables)
+    bt = torch.zeros(len(prompts), mb, dtype=torch.int32)
+    for b, blks in enumerate(block_tables):
+        bt[b, :len(blks)] = torch.tensor(blks, dtype=torch.int32)
+    tiles = ops.attention_tiles([len(t) for t in prompts], hq, hkv, nqt)
+    nsplit = ops.pick_nsplit(len(tiles) * hkv, max(ctx)) if prompts else 1
+    last = torch.tensor([q - 1 for q in qs[1:]], dtype=torch.int64)
+    it = lambda x: torch.tensor(x, dtype=torch.int32)  # noqa: E731
+    sb = StepBatch(it(ids), it(pos), it(tok_seq), bt, it(qs), it(ctx), last,
+                   torch.tensor(tiles, dtype=torch.int32).view(-1, 2), len(tiles), nqt, nsplit)
+    return to_device(sb, device)
+
+
+def to_device(sb: StepBatch, device) -> StepBatch:
+    mv = lambda t: None if t is None else t.to(device, non_blocking=True)  # noqa: E731
+    return StepBatch(mv(sb.ids), mv(sb.pos), mv(sb.tok_seq), mv(sb.block_table), mv(sb.q_start), mv(sb.ctx_len),
+                     mv(sb.last_idx), mv(sb.tiles), sb.ntiles, sb.nqt, sb.nsplit)
+
+
+# -----------------------------------------------------------------------------------------------------------------
+# model
+# -----------------------------------------------------------------------------------------------------------------
+
+
+class LlamaModel:
+    def __init__(self, cfg: LlamaConfig, weights: LlamaWeights, tp: TPContext | None = None, device="cpu",
+                 max_position: int | None = None):
+        self.cfg, self.w = cfg, weights
+        self.tp = tp or TPContext.single()
+        self.device = torch.device(device)
+        self.hq, self.hkv = _local_heads(cfg, self.tp)
+        self.cos_sin = rope_table(cfg, max_position or cfg.max_position, self.device)
+        self.scale = 1.0 / math.sqrt(cfg.head_dim)
+
+    def forward(self, sb: StepBatch, kv: KVCache, logits_dtype=torch.bfloat16) -> torch.Tensor:
+        """Returns logits [B, V] for the token at sb.last_idx of every sequence (full vocab on every TP rank)."""
+        cfg, w, tp = self.cfg, self.w, self.tp
+        T = sb.ids.numel()
+        eps = cfg.rms_eps
+        h = ops.embedding(sb.ids, w.embed, w.vocab_start)
+        h = tp.all_reduce(h)
+        resid = h
+        x = ops.rmsnorm(h, w.layers[0].attn_norm, eps)
+        q_buf = torch.empty(T, self.hq, cfg.head_dim, device=h.device, dtype=h.dtype)
+        for li, lw in enumerate(w.layers):
+            qkv = ops.linear(x, lw.wqkv)
+            ops.rope_kv_write(qkv, sb.pos, sb.tok_seq, sb.block_table, self.cos_sin, q_buf, kv.k[li], kv.v[li],
+                              self.hq, self.hkv, True)
+            attn = ops.paged_attention(q_buf, kv.k[li], kv.v[li], sb.block_table, sb.q_start, sb.ctx_len, sb.tiles,
+                                       sb.ntiles, sb.nqt, sb.nsplit, self.scale)
+            o = tp.all_reduce(ops.linear(attn.view(T, -1), lw.wo))
+            x = ops.add_rmsnorm(o, resid, lw.mlp_norm, eps)
+            a = ops.silu_mul(ops.linear(x, lw.w_gu))
+            dn = tp.all_reduce(ops.linear(a, lw.w_down))
+            if li + 1 < len(w.layers):
+                x = ops.add_rmsnorm(dn, resid, w.layers[li + 1].attn_norm, eps)
+            else:  # only the sampled rows need the final norm + LM head
+                dl = dn.index_select(0, sb.last_idx)
+                rl = resid.index_select(0, sb.last_idx)
+                x = ops.add_rmsnorm(dl, rl, w.norm, eps)
+        logits = ops.linear(x, w.lm_head)
+        logits = tp.all_gather_last(logits)
+        return logits if logits.dtype == logits_dtype else logits.to(logits_dtype)
+
+
+def build_model(preset: str | LlamaConfig = "tiny", device="cpu", tp: TPContext | None = None, seed: int = 0,
+                checkpoint: str | None = None, max_position: int | None = None) -> LlamaModel:
+    tp = tp or TPContext.single()
+    if checkpoint:
+        cfg, w = load_checkpoint(checkpoint, tp, device)
+    else:
+        cfg = preset if isinstance(preset, LlamaConfig) else get_config(preset)
+        w = random_weights(cfg, tp, device, seed)
+    return LlamaModel(cfg, w, tp, device, max_position)
+
+
+def config_dict(cfg: LlamaConfig) -> dict:
+    return asdict(cfg)

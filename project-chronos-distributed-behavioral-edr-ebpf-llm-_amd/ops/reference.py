@@ -1,0 +1,132 @@
+"""Pure-PyTorch reference implementations of every HIP kernel (the numerics oracle, and the CPU execution path).
+
+Each function mirrors the exact contract of its kernel in csrc/kernels (same layouts, same in-place semantics) and
+computes in fp32, rounding to bf16 at the same points the kernel and HF Llama do.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+
+def embedding(ids: torch.Tensor, table: torch.Tensor, vstart: int = 0) -> torch.Tensor:
+    idx = ids.long() - vstart
+    ok = (idx >= 0) & (idx < table.shape[0])
+    out = table[idx.clamp(0, table.shape[0] - 1)]
+    return out * ok[:, None].to(out.dtype)
+
+
+def rmsnorm(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+    xf = x.float()
+    inv = torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + eps)
+    return (xf * inv).to(torch.bfloat16).float().mul(w.float()).to(x.dtype)
+
+
+def add_rmsnorm(x: torch.Tensor, resid: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+    resid.copy_((x.float() + resid.float()).to(resid.dtype))
+    return rmsnorm(resid, w, eps)
+
+
+def silu_mul(gu: torch.Tensor) -> torch.Tensor:
+    f = gu.shape[-1] // 2
+    g, u = gu[..., :f].float(), gu[..., f:].float()
+    return (torch.nn.functional.silu(g).to(torch.bfloat16).float() * u).to(gu.dtype)
+
+
+def rope_kv_write(qkv, pos, tok_seq, block_table, cos_sin, q_out, k_cache, v_cache, hq: int, hkv: int,
+                  write_q: bool = True) -> None:
+    T = qkv.shape[0]
+    D = 128
+    x = qkv.view(T, hq + 2 * hkv, D).float()
+    p = pos.long()
+    cos = cos_sin[p, :64].float()[:, None, :]
+    sin = cos_sin[p, 64:].float()[:, None, :]
+    qk = x[:, : hq + hkv]
+    x1, x2 = qk[..., :64], qk[..., 64:]
+    rot = torch.cat([x1 * cos - x2 * sin, x2 * cos + x1 * sin], dim=-1).to(torch.bfloat16)
+    if write_q:
+        q_out.view(-1, hq, D)[:T].copy_(rot[:, :hq])
+    bs = k_cache.shape[2]
+    blk = block_table[tok_seq.long(), p // bs].long()
+    off = p % bs
+    k_cache[blk, :, off, :] = rot[:, hq:]
+    v = x[:, hq + hkv:].to(torch.bfloat16)  # [T, hkv, D]
+    v_cache[blk, :, :, off] = v
+
+
+def paged_attention(q, k_cache, v_cache, block_table, q_start, ctx_len, tiles=None, ntiles=0, nqt=1, nsplit=1,
+                    scale: float | None = None) -> torch.Tensor:
+    """Causal varlen attention over the paged cache.  q [T, Hq, 128]; seqs given by q_start/ctx_len."""
+    T, hq, D = q.shape
+    hkv, bs = k_cache.shape[1], k_cache.shape[2]
+    G = hq // hkv
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    out = torch.zeros_like(q)
+    if tiles is None:  # decode: one token per sequence, seq i = token i
+        qs = list(range(ntiles + 1))
+    else:
+        qs = q_start.tolist()
+    B = len(qs) - 1
+    bt = block_table.long()
+    for b in range(B):
+        q0, q1 = qs[b], qs[b + 1]
+        ql = q1 - q0
+        if ql == 0:
+            continue
+        ctx = int(ctx_len[b])
+        nblk = (ctx + bs - 1) // bs
+        blks = bt[b, :nblk]
+        K = k_cache[blks].permute(1, 0, 2, 3).reshape(hkv, nblk * bs, D)[:, :ctx].float()
+        V = v_cache[blks].permute(1, 0, 3, 2).reshape(hkv, nblk * bs, D)[:, :ctx].float()
+        qq = q[q0:q1].float().view(ql, hkv, G, D)
+        s = torch.einsum("qhgd,hkd->hgqk", qq, K) * scale
+        qpos = torch.arange(ctx - ql, ctx, device=q.device)
+        kpos = torch.arange(ctx, device=q.device)
+        mask = kpos[None, :] > qpos[:, None]
+        s = s.masked_fill(mask[None, None], float("-inf"))
+        p = torch.softmax(s, dim=-1)
+        o = torch.einsum("hgqk,hkd->qhgd", p, V)
+        out[q0:q1] = o.reshape(ql, hq, D).to(q.dtype)
+    return out
+
+
+def constrained_sample(logits, row_of_slot, next_tab, dist, done_state: int, state, remaining, temperature, seed,
+                       ids, pos, ctx, nout, out_tokens) -> None:
+    """Greedy / Gumbel-max sampling restricted by the token DFA; advances the slot state in place (host loop)."""
+    n = state.numel()
+    V = next_tab.shape[1]
+    for slot in range(n):
+        s = int(state[slot])
+        if s < 0 or s == done_state:
+            continue
+        row = int(row_of_slot[slot]) if row_of_slot is not None else slot
+        if row < 0:
+            continue
+        nx = next_tab[s].long()
+        budget = int(remaining[slot]) - 1
+        legal = (nx >= 0)
+        legal &= dist[nx.clamp(min=0)].long() <= budget
+        if not bool(legal.any()):
+            state[slot] = done_state
+            continue
+        sc = logits[row, :V].float()
+        t = float(temperature[slot]) if temperature is not None else 0.0
+        if t > 0:
+            g = torch.Generator(device="cpu")
+            g.manual_seed((int(seed[slot]) if seed is not None else 0) * 1000003 + int(nout[slot]) * 7919 + slot)
+            u = torch.rand(V, generator=g).clamp_(1e-7, 1 - 1e-7).to(sc.device)
+            sc = sc / t - torch.log(-torch.log(u))
+        sc = sc.masked_fill(~legal, float("-inf"))
+        tok = int(torch.argmax(sc))
+        ns = int(nx[tok])
+        k = int(nout[slot])
+        if k < out_tokens.shape[1]:
+            out_tokens[slot, k] = tok
+        nout[slot] = k + 1
+        remaining[slot] = budget
+        state[slot] = ns
+        if ns != done_state:
+            ids[slot] = tok
+            pos[slot] += 1
+            ctx[slot] += 1

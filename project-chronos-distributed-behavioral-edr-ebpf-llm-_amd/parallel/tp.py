@@ -1,0 +1,57 @@
+"""Tensor-parallel context: the collectives the Llama forward needs.
+
+One process per GPU.  ``torch.distributed`` with backend ``"nccl"`` is RCCL on ROCm and runs over xGMI between the
+GPUs of a node; ``"gloo"`` serves the CPU tests.  Column-parallel wqkv / w_gu, row-parallel wo / w_down, vocab-parallel
+embedding and LM head, so a layer needs exactly two all-reduces (after o_proj and after down_proj).
+
+The small decode-time all-reduces (70B TP8: 160 per step at 16 KiB x batch) are latency-bound; ``allreduce`` lets a
+faster one-shot implementation (parallel/custom_ar.py) take messages under its size cap, RCCL takes the rest.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, Optional
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class TPContext:
+    rank: int = 0
+    world: int = 1
+    group: Optional[object] = None
+    fast_allreduce: Optional[Callable[[torch.Tensor], Optional[torch.Tensor]]] = None
+
+    @classmethod
+    def single(cls) -> "TPContext":
+        return cls()
+
+    @classmethod
+    def from_group(cls, group=None) -> "TPContext":
+        return cls(dist.get_rank(group), dist.get_world_size(group), group)
+
+    def all_reduce(self, x: torch.Tensor) -> torch.Tensor:
+        if self.world == 1:
+            return x
+        if self.fast_allreduce is not None:
+            y = self.fast_allreduce(x)
+            if y is not None:
+                return y
+        dist.all_reduce(x, group=self.group)
+        return x
+
+    def all_gather_last(self, x: torch.Tensor) -> torch.Tensor:
+        """[.., n] shards -> [.., n * world] (vocab-parallel logits)."""
+        if self.world == 1:
+            return x
+        parts = [torch.empty_like(x) for _ in range(self.world)]
+        dist.all_gather(parts, x.contiguous(), group=self.group)
+        return torch.cat(parts, dim=-1)
+
+    def broadcast_obj(self, obj, src: int = 0):
+        if self.world == 1:
+            return obj
+        box = [obj]
+        dist.broadcast_object_list(box, src=src, group=self.group)
+        return box[0]

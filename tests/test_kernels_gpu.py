@@ -1,0 +1,251 @@
+"""Numerics of every gfx950 HIP kernel vs its fp32 PyTorch reference (chronos.ops.reference).
+
+Run on a real MI355X: ``python -m pytest tests -m gpu``.  Inputs are asymmetric random data at odd shapes (GQA
+groups 4 and 8, page boundaries, varlen chunks with a cached prefix, partial last pages, split-K decode).
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    from chronos import ops
+
+    ops.load()
+    import chronos.native as n
+
+    assert "_C" in n._loaded, "HIP kernel library must be the one running"
+
+
+def _close(a, b, atol, rtol=0.0):
+    d = (a.float() - b.float()).abs()
+    lim = atol + rtol * b.float().abs()
+    assert bool((d <= lim).all()), f"max err {float(d.max()):.4g}"
+
+
+@pytest.mark.parametrize("rows,d", [(1, 4096), (37, 4096), (5, 8192), (3, 256), (2, 1024)])
+def test_rmsnorm(rows, d):
+    from chronos import ops
+    from chronos.ops import reference as ref
+
+    g = torch.Generator(device=DEV).manual_seed(rows * d)
+    x = torch.randn(rows, d, device=DEV, generator=g).to(torch.bfloat16) * 3 + 0.5
+    w = torch.rand(d, device=DEV, generator=g).to(torch.bfloat16) + 0.5
+    _close(ops.rmsnorm(x, w, 1e-5), ref.rmsnorm(x, w, 1e-5), 1e-2, 1e-2)
+    r1 = torch.randn(rows, d, device=DEV, generator=g).to(torch.bfloat16)
+    r2 = r1.clone()
+    y1 = ops.add_rmsnorm(x, r1, w, 1e-5)
+    y2 = ref.add_rmsnorm(x, r2, w, 1e-5)
+    assert torch.equal(r1, r2)
+    _close(y1, y2, 1e-2, 1e-2)
+
+
+def test_silu_mul_and_embedding():
+    from chronos import ops
+    from chronos.ops import reference as ref
+
+    g = torch.Generator(device=DEV).manual_seed(1)
+    gu = (torch.randn(19, 2 * 1408, device=DEV, generator=g) * 4).to(torch.bfloat16)
+    _close(ops.silu_mul(gu), ref.silu_mul(gu), 2e-2, 1e-2)
+    table = torch.randn(1000, 512, device=DEV, generator=g).to(torch.bfloat16)
+    ids = torch.tensor([0, 999, 5, 500, 1200, -3 + 2000], dtype=torch.int32, device=DEV)
+    assert torch.equal(ops.embedding(ids, table, 0), ref.embedding(ids, table, 0))
+    assert torch.equal(ops.embedding(ids, table, 500), ref.embedding(ids, table, 500))
+
+
+def _cache(nb, hkv, bs, g):
+    k = (torch.randn(nb, hkv, bs, 128, device=DEV, generator=g)).to(torch.bfloat16)
+    v = (torch.randn(nb, hkv, 128, bs, device=DEV, generator=g)).to(torch.bfloat16)
+    return k, v
+
+
+@pytest.mark.parametrize("hq,hkv,bs", [(32, 8, 16), (8, 1, 32), (4, 2, 16)])
+def test_rope_kv_write(hq, hkv, bs):
+    from chronos import ops
+    from chronos.models.llama import get_config, rope_table
+    from chronos.ops import reference as ref
+
+    g = torch.Generator(device=DEV).manual_seed(hq)
+    T = 45
+    cs = rope_table(get_config("llama3.1-8b"), 4096, DEV)
+    qkv = torch.randn(T, (hq + 2 * hkv) * 128, device=DEV, generator=g).to(torch.bfloat16)
+    pos = torch.randint(0, 4000, (T,), device=DEV, generator=g).to(torch.int32)
+    # distinct slots: token t -> block perm[t], offset t % bs
+    nb = 64
+    bt = torch.randperm(nb, device=DEV, generator=g).to(torch.int32).view(1, nb)
+    pos = (torch.arange(T, device=DEV) * 7 % (nb * bs)).to(torch.int32)
+    tok_seq = torch.zeros(T, dtype=torch.int32, device=DEV)
+    k1, v1 = _cache(nb, hkv, bs, g)
+    k2, v2 = k1.clone(), v1.clone()
+    q1 = torch.empty(T, hq, 128, device=DEV, dtype=torch.bfloat16)
+    q2 = torch.empty_like(q1)
+    ops.rope_kv_write(qkv, pos, tok_seq, bt, cs, q1, k1, v1, hq, hkv, True)
+    ref.rope_kv_write(qkv, pos, tok_seq, bt, cs, q2, k2, v2, hq, hkv, True)
+    _close(q1, q2, 2e-2, 1e-2)
+    _close(k1, k2, 2e-2, 1e-2)
+    assert torch.equal(v1, v2)
+
+
+def _attn_case(q_lens, ctx_lens, hq, hkv, bs, seed):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    B = len(q_lens)
+    nbs = [(c + bs - 1) // bs for c in ctx_lens]
+    nb = sum(nbs) + 3
+    k, v = _cache(nb, hkv, bs, g)
+    perm = torch.randperm(nb, device=DEV, generator=g).tolist()
+    mb = max(nbs)
+    bt = torch.zeros(B, mb, dtype=torch.int32)
+    o = 0
+    for b, n in enumerate(nbs):
+        bt[b, :n] = torch.tensor(perm[o:o + n])
+        o += n
+    T = sum(q_lens)
+    q = (torch.randn(T, hq, 128, device=DEV, generator=g) * 2).to(torch.bfloat16)
+    qs = [0]
+    for n in q_lens:
+        qs.append(qs[-1] + n)
+    return q, k, v, bt.to(DEV), torch.tensor(qs, dtype=torch.int32, device=DEV), \
+        torch.tensor(ctx_lens, dtype=torch.int32, device=DEV)
+
+
+@pytest.mark.parametrize("nqt", [1, 2])
+@pytest.mark.parametrize("hq,hkv,bs", [(32, 8, 16), (16, 2, 16), (8, 1, 32)])
+@pytest.mark.parametrize("nsplit", [1, 3])
+def test_paged_attention_prefill(nqt, hq, hkv, bs, nsplit):
+    from chronos import ops
+    from chronos.ops import reference as ref
+
+    q_lens = [1, 17, 64, 5, 100]
+    ctx_lens = [1, 17, 200, 37, 100]  # seq 2 and 3 have a cached prefix (chunked prefill)
+    q, k, v, bt, qs, ctx = _attn_case(q_lens, ctx_lens, hq, hkv, bs, seed=hq + nqt)
+    tiles = ops.attention_tiles(q_lens, hq, hkv, nqt)
+    tt = torch.tensor(tiles, dtype=torch.int32, device=DEV).view(-1, 2)
+    out = ops.paged_attention(q, k, v, bt, qs, ctx, tt, len(tiles), nqt, nsplit)
+    exp = ref.paged_attention(q, k, v, bt, qs, ctx, tt, len(tiles), nqt, nsplit)
+    _close(out, exp, 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8), (8, 1)])
+@pytest.mark.parametrize("nsplit", [1, 4, 16])
+def test_paged_attention_decode(hq, hkv, nsplit):
+    from chronos import ops
+    from chronos.ops import reference as ref
+
+    ctx_lens = [1, 15, 16, 33, 511, 1000, 2049]
+    q, k, v, bt, qs, ctx = _attn_case([1] * len(ctx_lens), ctx_lens, hq, hkv, 16, seed=hq * nsplit)
+    out = ops.paged_attention(q, k, v, bt, qs, ctx, None, len(ctx_lens), 1, nsplit)
+    exp = ref.paged_attention(q, k, v, bt, qs, ctx, None, len(ctx_lens), 1, nsplit)
+    _close(out, exp, 2e-2, 2e-2)
+
+
+def test_paged_attention_spike_rescale():
+    """Force the online-softmax rescale: one key dominates late in a long context."""
+    from chronos import ops
+    from chronos.ops import reference as ref
+
+    q, k, v, bt, qs, ctx = _attn_case([1, 1], [700, 300], 32, 8, 16, seed=9)
+    # spike key 650 of seq 0 (block index 650 // 16 of its table) against q head 0's direction
+    blk = int(bt[0, 650 // 16])
+    k[blk, 0, 650 % 16] = (q[0, 0].float() * 4).to(torch.bfloat16)
+    out = ops.paged_attention(q, k, v, bt, qs, ctx, None, 2, 1, 1)
+    exp = ref.paged_attention(q, k, v, bt, qs, ctx, None, 2, 1, 1)
+    _close(out, exp, 2e-2, 2e-2)
+
+
+def test_constrained_sample_matches_reference():
+    from chronos import ops
+    from chronos.brain.constrain import DONE, GrammarBank
+    from chronos.brain.tokenizer import ChronosBPE
+    from chronos.ops import reference as ref
+    from chronos.sensor.prompt import VERDICT_SCHEMA
+
+    tok = ChronosBPE()
+    bank = GrammarBank(tok.token_bytes_list(), tok.stop_ids, 128256, 1024, DEV)
+    gs = bank.get(VERDICT_SCHEMA)
+    gj = bank.get("json")
+    S = 6
+    g = torch.Generator(device=DEV).manual_seed(3)
+    i32 = dict(dtype=torch.int32, device=DEV)
+    state = torch.tensor([gs.start, gj.start, -1, gs.start, gj.start, gs.start], **i32)
+    rem = torch.tensor([40, 30, 5, 16, 3, 40], **i32)
+    temp = torch.tensor([0, 0, 0, 0.7, 0, 1.3], dtype=torch.float32, device=DEV)
+    seed = torch.arange(S, **i32)
+    bufs1 = [torch.zeros(S, **i32) for _ in range(4)] + [torch.zeros(S, 64, **i32)]
+    bufs2 = [b.clone() for b in bufs1]
+    st1, st2 = state.clone(), state.clone()
+    r1, r2 = rem.clone(), rem.clone()
+    for step in range(45):
+        logits = (torch.randn(S, 128256, device=DEV, generator=g) * 3).to(torch.bfloat16)
+        ops.constrained_sample(logits, None, bank.next, bank.dist, DONE, st1, r1, temp, seed, *bufs1)
+        # reference on greedy rows only (the Gumbel RNG streams differ by design)
+        greedy = (temp == 0)
+        st2g = torch.where(greedy, st2, torch.full_like(st2, -1))
+        ref.constrained_sample(logits, None, bank.next, bank.dist, DONE, st2g, r2, temp, seed, *bufs2)
+        st2 = torch.where(greedy, st2g, st1)
+        r2 = torch.where(greedy, r2, r1)
+        assert torch.equal(st1[greedy], st2[greedy]), step
+    nout = bufs1[3]
+    out = bufs1[4]
+    assert torch.equal(out[temp == 0], bufs2[4][temp == 0])
+    # every non-empty row finished within its budget with a grammar-valid string
+    import json
+
+    for s in [0, 1, 3, 4, 5]:
+        assert int(st1[s]) == DONE, s
+        ids = out[s, : int(nout[s])].tolist()
+        assert ids[-1] in tok.stop_ids
+        text = tok.decode(ids[:-1])
+        json.loads(text)
+        assert int(nout[s]) <= int(rem[s])
+
+
+def test_model_gpu_matches_cpu_reference():
+    from chronos.models.llama import KVCache, build_model, make_prefill_batch
+
+    torch.manual_seed(0)
+    mg = build_model("tiny", DEV, seed=5)
+    mc = build_model("tiny", "cpu", seed=5)
+    # same weights (generated on different devices) -> copy GPU weights to CPU model
+    for lg, lc in zip(mg.w.layers, mc.w.layers):
+        for n in ("attn_norm", "wqkv", "wo", "mlp_norm", "w_gu", "w_down"):
+            getattr(lc, n).copy_(getattr(lg, n).cpu())
+    mc.w.embed.copy_(mg.w.embed.cpu())
+    mc.w.lm_head.copy_(mg.w.lm_head.cpu())
+    prompts = [[128000 + 0] + list(range(10, 40)), list(range(100, 113))]
+    bts = [[1, 2, 3], [4]]
+    kvg = KVCache(mg.cfg, mg.tp, 8, 16, DEV)
+    kvc = KVCache(mc.cfg, mc.tp, 8, 16, "cpu")
+    sbg = make_prefill_batch(prompts, [0, 0], bts, mg.cfg, mg.tp, DEV, max_blocks=3)
+    sbc = make_prefill_batch(prompts, [0, 0], bts, mc.cfg, mc.tp, "cpu", max_blocks=3)
+    lg = mg.forward(sbg, kvg).float().cpu()
+    lc = mc.forward(sbc, kvc).float()
+    assert (lg - lc).abs().max() < 0.05 * lc.abs().max() + 0.05
+    assert (lg.argmax(-1) == lc.argmax(-1)).float().mean() >= 0.5
+
+
+def test_engine_graph_equals_eager():
+    from chronos.brain.engine.engine import Engine, EngineConfig
+    from chronos.sensor.prompt import VERDICT_SCHEMA, build_prompt
+
+    chains = [["[OPEN] attack_chain.sh -> /tmp/malware.bin", "[EXEC] attack_chain.sh -> curl"],
+              ["[EXEC] bash -> chmod", "[OPEN] chmod -> /tmp/x", "[EXEC] bash -> cat"],
+              ["[OPEN] sshd -> /var/log/auth.log", "[EXEC] sshd -> bash"]]
+    outs = []
+    for graphs in (True, False):
+        eng = Engine(EngineConfig(model="small", device=DEV, max_slots=4, max_model_len=256, use_graphs=graphs,
+                                  decode_burst=4))
+        reqs = [eng.submit(build_prompt(c), fmt=VERDICT_SCHEMA, num_predict=48) for c in chains]
+        eng.run_until_idle()
+        outs.append([r.out_ids for r in reqs])
+        import json
+
+        for r in reqs:
+            v = json.loads(r.text)
+            assert {"risk_score", "verdict", "reason"} <= set(v)
+    assert outs[0] == outs[1]
