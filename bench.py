@@ -77,13 +77,21 @@ def main():
         if cuda:
             torch.cuda.synchronize()
 
+    def progress(msg):
+        if rank == 0:
+            print(f"[bench] {time.strftime('%H:%M:%S')} {msg}", file=sys.stderr, flush=True)
+
+    progress(f"engine ready: kv blocks {eng.blocks.num_blocks}, load {eng.load_seconds:.1f}s")
     for s in range(a.warmup):
+        t = time.perf_counter()
         run_step(prompts[s * a.streams:(s + 1) * a.streams])
+        progress(f"warmup step {s}: {time.perf_counter() - t:.2f}s {dict(eng.stats)}")
     barrier()
     t0 = time.perf_counter()
     timed = []
     for s in range(a.warmup, total_steps):
         timed += run_step(prompts[s * a.streams:(s + 1) * a.streams])
+        progress(f"step {s} done")
     barrier()
     elapsed = time.perf_counter() - t0
 

@@ -4,8 +4,9 @@
 // can fault the whole GPU box), launches on the current HIP stream (so ops are hipGraph-capturable), and never
 // allocates inside a captured region except through torch's caching allocator.
 #include <ATen/ATen.h>
-#include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
+// ROCm torch presents HIP devices as DeviceType::CUDA ("masquerading"): guards/streams must use these forms.
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <torch/library.h>
 
 #include <hip/hip_runtime.h>
@@ -30,7 +31,7 @@ namespace {
 
 using at::Tensor;
 
-inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+inline hipStream_t cur_stream() { return c10::hip::getCurrentHIPStreamMasqueradingAsCUDA().stream(); }
 inline const uint16_t* bf(const Tensor& t) { return reinterpret_cast<const uint16_t*>(t.data_ptr()); }
 inline uint16_t* bfm(const Tensor& t) { return reinterpret_cast<uint16_t*>(t.data_ptr()); }
 inline const int32_t* i32(const Tensor& t) { return t.data_ptr<int32_t>(); }
@@ -54,7 +55,7 @@ Tensor embedding(const Tensor& ids, const Tensor& table, int64_t vstart) {
     chk_i32(ids, "ids");
     chk_bf16(table, "table");
     CHK(table.dim() == 2 && table.size(1) % 8 == 0, "table must be [V, d] with d % 8 == 0");
-    c10::hip::HIPGuard g(ids.device());
+    c10::hip::HIPGuardMasqueradingAsCUDA g(ids.device());
     auto out = at::empty({ids.numel(), table.size(1)}, table.options());
     chronos::launch_embedding(i32(ids), bf(table), bfm(out), (int)ids.numel(), (int)table.size(1), vstart,
                               table.size(0), cur_stream());
@@ -66,7 +67,7 @@ Tensor rmsnorm(const Tensor& x, const Tensor& w, double eps) {
     chk_bf16(w, "w");
     const int64_t d = x.size(-1);
     CHK(w.numel() == d && d % 8 == 0 && d <= 16384, "rmsnorm: d must match w, be % 8 and <= 16384");
-    c10::hip::HIPGuard g(x.device());
+    c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
     auto y = at::empty_like(x);
     chronos::launch_rmsnorm(bf(x), nullptr, bf(w), bfm(y), (int)(x.numel() / d), (int)d, (float)eps, cur_stream());
     return y;
@@ -80,7 +81,7 @@ Tensor add_rmsnorm(const Tensor& x, const Tensor& resid, const Tensor& w, double
     const int64_t d = x.size(-1);
     CHK(resid.sizes() == x.sizes(), "add_rmsnorm: shape mismatch");
     CHK(w.numel() == d && d % 8 == 0 && d <= 16384, "add_rmsnorm: d must match w, be % 8 and <= 16384");
-    c10::hip::HIPGuard g(x.device());
+    c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
     auto y = at::empty_like(x);
     chronos::launch_rmsnorm(bf(x), bfm(resid), bf(w), bfm(y), (int)(x.numel() / d), (int)d, (float)eps, cur_stream());
     return y;
@@ -106,7 +107,7 @@ void rope_kv_write(const Tensor& qkv, const Tensor& pos, const Tensor& tok_seq, 
     CHK(v_cache.dim() == 4 && v_cache.size(1) == hkv && v_cache.size(2) == 128 && v_cache.size(3) == k_cache.size(2),
         "v_cache [NB, hkv, 128, BS]");
     CHK(block_table.dim() == 2, "block_table [B, max_blocks]");
-    c10::hip::HIPGuard g(qkv.device());
+    c10::hip::HIPGuardMasqueradingAsCUDA g(qkv.device());
     chronos::launch_rope_kv_write(bf(qkv), i32(pos), i32(tok_seq), i32(block_table), (int)block_table.size(1),
                                   cos_sin.data_ptr<float>(), bfm(q_out), bfm(k_cache), bfm(v_cache), (int)t, (int)hq,
                                   (int)hkv, (int)k_cache.size(2), write_q ? 1 : 0, cur_stream());
@@ -116,7 +117,7 @@ Tensor silu_mul(const Tensor& gu) {
     chk_bf16(gu, "gate_up");
     const int64_t f2 = gu.size(-1);
     CHK(f2 % 16 == 0, "gate_up last dim must be 2F with F % 8 == 0");
-    c10::hip::HIPGuard g(gu.device());
+    c10::hip::HIPGuardMasqueradingAsCUDA g(gu.device());
     auto sizes = gu.sizes().vec();
     sizes.back() = f2 / 2;
     auto out = at::empty(sizes, gu.options());
@@ -148,7 +149,7 @@ Tensor paged_attention(const Tensor& q, const Tensor& k_cache, const Tensor& v_c
     } else {
         CHK(ctx_len.numel() >= ntiles && q.size(0) >= ntiles, "decode mode: one query token per tile");
     }
-    c10::hip::HIPGuard g(q.device());
+    c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
     auto out = at::empty_like(q);
     Tensor po, pl;
     if (nsplit > 1) {
@@ -200,7 +201,7 @@ void constrained_sample(const Tensor& logits, const c10::optional<Tensor>& row_o
         chk_i32(*seed, "seed");
         sp = i32(*seed);
     }
-    c10::hip::HIPGuard g(logits.device());
+    c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
     chronos::launch_constrained_sample(logits.data_ptr(), logits.scalar_type() == at::kFloat, logits.stride(0), rp,
                                        (int)n, (int)vocab, next.data_ptr<int16_t>(), dist.data_ptr<int16_t>(),
                                        (int)done_state, i32m(state), i32m(remaining), tp, sp, i32m(ids), i32m(pos),

@@ -100,6 +100,8 @@ class Engine:
         self.cfg = cfg
         self.tp = tp or TPContext.single()
         self.device = torch.device(cfg.device)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
             ops.load()  # the HIP library must load on a GPU engine — never a silent eager fallback
@@ -174,6 +176,11 @@ class Engine:
             req.start_state = self.bank.get(fmt).start
         except Exception as e:  # bad schema: report, never crash the engine
             req.error = f"invalid format: {e}"
+            self._finish(req, "error")
+            return req
+        need = self.bank.min_tokens(req.start_state)
+        if n < need:
+            req.error = f"num_predict={n} cannot fit the shortest output of this format ({need} tokens)"
             self._finish(req, "error")
             return req
         with self._lock:
