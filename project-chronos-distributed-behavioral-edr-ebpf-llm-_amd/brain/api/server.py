@@ -1,0 +1,207 @@
+"""Ollama-compatible HTTP front door of the Brain (reference README.md:57-62 `ollama serve`).
+
+Endpoints:
+  POST /api/generate   the sensor contract (chronos_sensor.py:117-120): stream=false -> one JSON object whose
+                       ``response`` is the (constrained) model text; stream=true -> NDJSON chunks (Ollama default)
+  POST /api/chat       Llama-3 chat template over ``messages``
+  GET  /api/tags, POST /api/show, GET /api/ps, GET /api/version, GET /      model listing / health (Ollama shapes)
+  GET  /healthz        liveness + engine state;   GET /metrics   Prometheus text (utils/metrics.py)
+
+Run: ``python -m chronos.brain.api --model llama3-8b --port 11434 [--dp N]`` (binds 0.0.0.0 like OLLAMA_HOST=0.0.0.0).
+Backends: EngineService (one engine on this process's GPU), DPRouter (one engine process per GPU), FakeBackend
+(tests / fault injection).
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import logging
+import time
+
+from aiohttp import web
+
+from ...utils.metrics import METRICS
+from .protocol import OLLAMA_VERSION, BadRequest, GenerateParams, chat_response, final_fields, generate_response, now_iso
+
+log = logging.getLogger("chronos.api")
+
+
+def make_app(backend, model_name: str = "llama3", request_timeout: float | None = None) -> web.Application:
+    app = web.Application(client_max_size=64 * 2**20)
+    started = time.time()
+
+    async def _params(request, chat=False) -> GenerateParams:
+        try:
+            body = await request.json()
+        except Exception:
+            raise web.HTTPBadRequest(text=json.dumps({"error": "invalid JSON body"}), content_type="application/json")
+        try:
+            return GenerateParams.parse(body, chat=chat)
+        except (BadRequest, ValueError, TypeError) as e:
+            raise web.HTTPBadRequest(text=json.dumps({"error": str(e)}), content_type="application/json")
+
+    async def _run(params, chat: bool, request):
+        model = params.model or model_name
+        if not params.stream:
+            try:
+                coro = backend.generate(params)
+                req = await (asyncio.wait_for(coro, request_timeout) if request_timeout else coro)
+            except asyncio.TimeoutError:
+                return web.json_response({"error": "generation timed out"}, status=504)
+            if getattr(req, "error", None):
+                return web.json_response({"error": req.error}, status=400)
+            return web.json_response(chat_response(model, req) if chat else generate_response(model, req))
+        resp = web.StreamResponse(headers={"Content-Type": "application/x-ndjson"})
+        await resp.prepare(request)
+        async for text, final in backend.generate_stream(params):
+            if final is None:
+                chunk = {"model": model, "created_at": now_iso()}
+                if chat:
+                    chunk["message"] = {"role": "assistant", "content": text}
+                else:
+                    chunk["response"] = text
+                chunk["done"] = False
+            else:
+                if getattr(final, "error", None):
+                    chunk = {"error": final.error}
+                else:
+                    chunk = {"model": model, "created_at": now_iso()}
+                    if chat:
+                        chunk["message"] = {"role": "assistant", "content": ""}
+                    else:
+                        chunk["response"] = ""
+                    chunk.update(final_fields(final))
+            await resp.write((json.dumps(chunk) + "\n").encode())
+        await resp.write_eof()
+        return resp
+
+    async def generate(request):
+        return await _run(await _params(request), False, request)
+
+    async def chat(request):
+        return await _run(await _params(request, chat=True), True, request)
+
+    def _model_entry():
+        info = backend.info() if hasattr(backend, "info") else {}
+        return {"name": f"{model_name}:latest", "model": f"{model_name}:latest", "modified_at": now_iso(),
+                "size": int(info.get("params", 0)) * 2, "digest": "chronos-random-init",
+                "details": {"format": "safetensors", "family": "llama", "families": ["llama"],
+                            "parameter_size": f"{info.get('params', 0) / 1e9:.1f}B", "quantization_level": "BF16"}}
+
+    async def tags(request):
+        return web.json_response({"models": [_model_entry()]})
+
+    async def ps(request):
+        e = _model_entry()
+        e["expires_at"] = "2999-01-01T00:00:00Z"  # weights stay resident (no keep_alive unload, quirk X8)
+        e["size_vram"] = e["size"]
+        return web.json_response({"models": [e]})
+
+    async def show(request):
+        info = backend.info() if hasattr(backend, "info") else {}
+        return web.json_response({"modelfile": "", "parameters": "", "template": "llama3",
+                                  "details": _model_entry()["details"], "model_info": info})
+
+    async def version(request):
+        return web.json_response({"version": OLLAMA_VERSION})
+
+    async def root(request):
+        return web.Response(text="Ollama is running")
+
+    async def healthz(request):
+        info = backend.info() if hasattr(backend, "info") else {}
+        return web.json_response({"status": "ok", "uptime_s": time.time() - started, **info})
+
+    async def metrics(request):
+        return web.Response(text=METRICS.render(), content_type="text/plain")
+
+    app.add_routes([
+        web.post("/api/generate", generate), web.post("/api/chat", chat), web.get("/api/tags", tags),
+        web.get("/api/ps", ps), web.post("/api/show", show), web.get("/api/version", version), web.get("/", root),
+        web.get("/healthz", healthz), web.get("/metrics", metrics),
+    ])
+    return app
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# fake backend (contract tests, fault injection: SURVEY.md §4.2 "contract" row, §5.3)
+# ---------------------------------------------------------------------------------------------------------------
+
+
+class FakeBackend:
+    """Answers every request with a canned verdict.  ``mode``: "ok", "stall" (sleep ``delay`` s), "raise",
+    "badjson" (response text that is not JSON), "error" (engine-level error)."""
+
+    def __init__(self, mode: str = "ok", delay: float = 0.0, verdict: dict | None = None):
+        self.mode, self.delay = mode, delay
+        self.verdict = verdict or {"risk_score": 8, "verdict": "MALICIOUS", "reason": "curl -> chmod -> exec dropper"}
+        self.seen: list[GenerateParams] = []
+
+    def _req(self, params):
+        from types import SimpleNamespace
+
+        now = time.perf_counter()
+        text = "not json {" if self.mode == "badjson" else json.dumps(self.verdict)
+        return SimpleNamespace(text=text, error="engine failure" if self.mode == "error" else None,
+                               prompt_ids=[0] * max(1, len(params.prompt) // 4), out_ids=[0] * 20, done_reason="stop",
+                               t_submit=now - 0.01, t_admit=now - 0.01, t_first=now - 0.005, t_done=now)
+
+    async def generate(self, params):
+        self.seen.append(params)
+        if self.mode == "stall":
+            await asyncio.sleep(self.delay)
+        if self.mode == "raise":
+            raise RuntimeError("injected fault")
+        return self._req(params)
+
+    async def generate_stream(self, params):
+        req = await self.generate(params)
+        for i in range(0, len(req.text), 8):
+            yield req.text[i:i + 8], None
+        yield "", req
+
+    def info(self):
+        return {"engines": 0, "model": "fake", "params": 0}
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# CLI
+# ---------------------------------------------------------------------------------------------------------------
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description="CHRONOS Brain: Ollama-compatible Llama-3 server on MI355X")
+    ap.add_argument("--host", default="0.0.0.0")
+    ap.add_argument("--port", type=int, default=11434)
+    ap.add_argument("--model", default="llama3-8b", help="preset (random-init) when --checkpoint is not given")
+    ap.add_argument("--checkpoint", default=None, help="HF or Meta Llama-3 checkpoint directory")
+    ap.add_argument("--tokenizer", default=None)
+    ap.add_argument("--served-name", default="llama3")
+    ap.add_argument("--dp", type=int, default=1, help="engine replicas, one process per GPU")
+    ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree per replica (torchrun launch)")
+    ap.add_argument("--max-slots", type=int, default=512)
+    ap.add_argument("--max-model-len", type=int, default=4096)
+    ap.add_argument("--device", default="cuda")
+    ap.add_argument("--fake", choices=["ok", "stall", "raise", "badjson"], default=None)
+    ap.add_argument("--jsonl", default=None, help="append per-request records here")
+    a = ap.parse_args(argv)
+    logging.basicConfig(level=logging.INFO)
+    METRICS.jsonl_path = a.jsonl
+    if a.fake:
+        backend = FakeBackend(a.fake, delay=60.0)
+    else:
+        from ..engine.engine import EngineConfig
+
+        cfg = EngineConfig(model=a.model, checkpoint=a.checkpoint, tokenizer=a.tokenizer, device=a.device,
+                           max_slots=a.max_slots, max_model_len=a.max_model_len)
+        if a.dp > 1:
+            from ...parallel.router import DPRouter
+
+            backend = DPRouter(cfg, a.dp)
+        else:
+            from .service import EngineService
+
+            backend = EngineService.from_config(cfg, a.served_name)
+    web.run_app(make_app(backend, a.served_name), host=a.host, port=a.port, access_log=None)
+    return 0

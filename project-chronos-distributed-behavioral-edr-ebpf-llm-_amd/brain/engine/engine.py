@@ -332,10 +332,22 @@ class Engine:
         n = self._decode_rows()
         st = self.s_state[:n].cpu()
         finished = [r for s, r in self.running.items() if int(st[s]) == DONE]
-        if not finished:
+        streaming = [r for r in self.running.values() if r.meta.get("on_tokens")]
+        if not finished and not streaming:
             return []
         nout = self.s_nout[:n].cpu()
         outs = self.s_out[:n].cpu()
+        for r in streaming:  # incremental tokens for stream=true clients
+            k = min(int(nout[r.slot]), self.cfg.max_out)
+            e = r.meta.get("emitted", 0)
+            if k > e:
+                r.meta["emitted"] = k
+                try:
+                    r.meta["on_tokens"](outs[r.slot, e:k].tolist())
+                except Exception:
+                    log.exception("stream callback failed")
+        if not finished:
+            return []
         now = time.perf_counter()
         reset = []
         for r in finished:

@@ -1,0 +1,161 @@
+"""Data-parallel replica router (SURVEY.md §2.5 "DP / replicas", §2.4 C7).
+
+For Llama-3-8B the best MI355X layout is one full replica per GPU (16 GB of weights next to 270 GB of KV per GPU, no
+collectives in steady state).  The router owns N worker processes — one per GPU, each with its own Engine, scheduler
+loop and HIP context — and dispatches every request to the replica with the fewest outstanding requests; results
+and streamed tokens come back over a multiprocessing queue.  The HTTP layer sees the same async interface as
+EngineService.
+"""
+from __future__ import annotations
+
+import asyncio
+import itertools
+import multiprocessing as mp
+import queue
+import threading
+import time
+from dataclasses import asdict
+from types import SimpleNamespace
+from typing import AsyncIterator, Optional
+
+
+def _worker(rank: int, cfg_dict: dict, req_q, res_q, device: str) -> None:
+    import torch
+
+    from ..brain.api.protocol import GenerateParams, chat_prompt_ids
+    from ..brain.engine.engine import Engine, EngineConfig
+
+    if device == "cuda":
+        torch.cuda.set_device(rank)
+        cfg_dict = dict(cfg_dict, device=f"cuda:{rank}")
+    eng = Engine(EngineConfig(**cfg_dict))
+    res_q.put(("ready", rank, None))
+
+    def finish(rid):
+        def cb(r):
+            res_q.put(("done", rid, dict(text=r.text, error=r.error, prompt_ids=len(r.prompt_ids),
+                                         out_ids=len(r.out_ids), done_reason=r.done_reason, t_submit=r.t_submit,
+                                         t_admit=r.t_admit, t_first=r.t_first, t_done=r.t_done, rank=rank)))
+        return cb
+
+    def tokens(rid):
+        return lambda ids: res_q.put(("tok", rid, ids))
+
+    stop = False
+    while not stop:
+        try:
+            item = req_q.get(timeout=0.05) if not eng.has_work() else req_q.get_nowait()
+        except queue.Empty:
+            item = None
+        while item is not None:
+            if item == "stop":
+                stop = True
+                break
+            rid, pd, stream = item
+            p = GenerateParams(**pd)
+            ids = chat_prompt_ids(eng.tok, p.messages) if p.messages is not None else \
+                eng.tok.chat_ids(p.prompt, system=p.system, raw=p.raw)
+            eng.submit(ids, fmt=p.format, num_predict=p.num_predict, temperature=p.temperature, seed=p.seed,
+                       callback=finish(rid), meta={"on_tokens": tokens(rid)} if stream else None)
+            try:
+                item = req_q.get_nowait()
+            except queue.Empty:
+                item = None
+        if eng.has_work():
+            eng.step()
+
+
+class DPRouter:
+    def __init__(self, cfg, replicas: int, device: str | None = None, start_timeout: float = 900.0):
+        self.n = replicas
+        dev = device or ("cuda" if str(cfg.device).startswith("cuda") else "cpu")
+        ctx = mp.get_context("spawn")
+        self._res = ctx.Queue()
+        self._reqs = [ctx.Queue() for _ in range(replicas)]
+        cfgd = asdict(cfg)
+        self._procs = [ctx.Process(target=_worker, args=(r, cfgd, self._reqs[r], self._res, dev), daemon=True)
+                       for r in range(replicas)]
+        for p in self._procs:
+            p.start()
+        ready = 0
+        t0 = time.time()
+        while ready < replicas:
+            kind, _, _ = self._res.get(timeout=max(1.0, start_timeout - (time.time() - t0)))
+            ready += kind == "ready"
+        self.outstanding = [0] * replicas
+        self._waiters: dict[int, tuple] = {}
+        self._rid = itertools.count()
+        self._lock = threading.Lock()
+        self._reader = threading.Thread(target=self._read, daemon=True)
+        self._reader.start()
+
+    def _read(self) -> None:
+        while True:
+            try:
+                kind, rid, val = self._res.get()
+            except (EOFError, OSError):
+                return
+            with self._lock:
+                w = self._waiters.get(rid)
+                if kind == "done":
+                    self._waiters.pop(rid, None)
+                    if w is not None:
+                        self.outstanding[w[2]] -= 1
+            if w is None:
+                continue
+            loop, sink, _ = w
+            loop.call_soon_threadsafe(sink, kind, val)
+
+    def _dispatch(self, params, stream: bool, sink) -> None:
+        loop = asyncio.get_running_loop()
+        with self._lock:
+            r = min(range(self.n), key=lambda i: self.outstanding[i])
+            self.outstanding[r] += 1
+            rid = next(self._rid)
+            self._waiters[rid] = (loop, sink, r)
+        self._reqs[r].put((rid, asdict(params), stream))
+
+    @staticmethod
+    def _result(val: dict) -> SimpleNamespace:
+        v = dict(val)
+        v["prompt_ids"] = [0] * v["prompt_ids"]
+        v["out_ids"] = [0] * v["out_ids"]
+        return SimpleNamespace(**v)
+
+    async def generate(self, params):
+        fut = asyncio.get_running_loop().create_future()
+
+        def sink(kind, val):
+            if kind == "done" and not fut.done():
+                fut.set_result(self._result(val))
+
+        self._dispatch(params, False, sink)
+        return await fut
+
+    async def generate_stream(self, params) -> AsyncIterator[tuple[str, Optional[object]]]:
+        aq: asyncio.Queue = asyncio.Queue()
+        self._dispatch(params, True, lambda kind, val: aq.put_nowait((kind, val)))
+        from ..brain.tokenizer import load_tokenizer
+
+        tok = getattr(self, "_tok", None) or load_tokenizer(None)
+        self._tok = tok
+        while True:
+            kind, val = await aq.get()
+            if kind == "tok":
+                text = tok.decode([i for i in val if i not in tok.stop_ids])
+                if text:
+                    yield text, None
+            else:
+                yield "", self._result(val)
+                return
+
+    def info(self) -> dict:
+        return {"engines": self.n, "outstanding": list(self.outstanding)}
+
+    def close(self) -> None:
+        for q in self._reqs:
+            q.put("stop")
+        for p in self._procs:
+            p.join(timeout=10)
+            if p.is_alive():
+                p.terminate()

@@ -1,0 +1,182 @@
+"""Sensor <-> Brain REST contract tests (SURVEY.md §4.2 "contract" row, App. A).
+
+A real aiohttp server on 127.0.0.1 is driven by the sensor's own clients (chronos.sensor.client), so the bytes on the
+wire are exactly what the reference sends (chronos_sensor.py:117-119) and reads (:120).
+"""
+import asyncio
+import json
+import socket
+import threading
+import time
+
+import pytest
+import requests
+
+from chronos.brain.api.server import FakeBackend, make_app
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+class Server:
+    def __init__(self, backend, **kw):
+        from aiohttp import web
+
+        self.port = _port()
+        self.loop = asyncio.new_event_loop()
+        self.backend = backend
+        app = make_app(backend, **kw)
+        self.runner = web.AppRunner(app)
+        ready = threading.Event()
+
+        def run():
+            asyncio.set_event_loop(self.loop)
+            self.loop.run_until_complete(self.runner.setup())
+            site = web.TCPSite(self.runner, "127.0.0.1", self.port)
+            self.loop.run_until_complete(site.start())
+            ready.set()
+            self.loop.run_forever()
+
+        self.t = threading.Thread(target=run, daemon=True)
+        self.t.start()
+        ready.wait(10)
+        self.url = f"http://127.0.0.1:{self.port}"
+
+    def close(self):
+        async def stop():
+            await self.runner.cleanup()
+
+        asyncio.run_coroutine_threadsafe(stop(), self.loop).result(10)
+        self.loop.call_soon_threadsafe(self.loop.stop)
+        self.t.join(5)
+
+
+@pytest.fixture
+def fake():
+    s = Server(FakeBackend("ok"))
+    yield s
+    s.close()
+
+
+def test_reference_request_roundtrip(fake):
+    """The exact reference call: requests.post(json={...,"stream": False,"format":"json"}) -> json.loads(response)."""
+    from chronos.sensor.prompt import build_prompt
+
+    prompt = build_prompt(["[OPEN] attack_chain.sh -> /tmp/malware.bin", "[EXEC] attack_chain.sh -> curl"])
+    resp = requests.post(f"{fake.url}/api/generate",
+                         json={"model": "llama3", "prompt": prompt, "stream": False, "format": "json"}, timeout=30)
+    body = resp.json()
+    verdict = json.loads(body["response"])
+    assert verdict["verdict"] == "MALICIOUS" and verdict["risk_score"] == 8
+    for k in ("model", "created_at", "done", "done_reason", "total_duration", "prompt_eval_count", "eval_count",
+              "eval_duration"):
+        assert k in body
+    seen = fake.backend.seen[-1]
+    assert seen.prompt == prompt and seen.format == "json" and seen.stream is False
+
+
+def test_sensor_clients_against_server(fake):
+    from chronos.sensor.client import AsyncBrainClient, BrainClient, ClientConfig
+
+    cfg = ClientConfig(url=f"{fake.url}/api/generate")
+    v = BrainClient(cfg).analyze(["[EXEC] bash -> curl", "[OPEN] curl -> /tmp/x"])
+    assert v["verdict"] == "MALICIOUS"
+
+    async def many():
+        c = AsyncBrainClient(cfg, max_inflight=16)
+        out = await asyncio.gather(*[c.analyze([f"[EXEC] bash -> cat{i}", "[OPEN] cat -> /etc/passwd"])
+                                     for i in range(40)])
+        await c.close()
+        return out
+
+    out = asyncio.run(many())
+    assert len(out) == 40 and all(o["verdict"] == "MALICIOUS" for o in out)
+
+
+def test_streaming_and_endpoints(fake):
+    r = requests.post(f"{fake.url}/api/generate", json={"prompt": "x", "format": "json"}, stream=True, timeout=30)
+    lines = [json.loads(l) for l in r.iter_lines() if l]
+    assert lines[-1]["done"] is True and all(not l["done"] for l in lines[:-1])
+    text = "".join(l["response"] for l in lines)
+    assert json.loads(text)["verdict"] == "MALICIOUS"
+    chat = requests.post(f"{fake.url}/api/chat", json={"messages": [{"role": "user", "content": "hi"}],
+                                                       "stream": False}, timeout=30).json()
+    assert chat["message"]["role"] == "assistant"
+    assert requests.get(f"{fake.url}/api/tags", timeout=5).json()["models"][0]["name"] == "llama3:latest"
+    assert "version" in requests.get(f"{fake.url}/api/version", timeout=5).json()
+    assert requests.get(f"{fake.url}/", timeout=5).text == "Ollama is running"
+    assert requests.get(f"{fake.url}/healthz", timeout=5).json()["status"] == "ok"
+    assert "chronos_requests_total" in requests.get(f"{fake.url}/metrics", timeout=5).text
+    bad = requests.post(f"{fake.url}/api/generate", json={"prompt": "x", "format": 7}, timeout=5)
+    assert bad.status_code == 400
+    bad = requests.post(f"{fake.url}/api/generate", data=b"{not json", timeout=5)
+    assert bad.status_code == 400
+
+
+@pytest.mark.parametrize("mode", ["stall", "badjson"])
+def test_fault_injection_maps_to_error_verdict(mode):
+    """Reference quirk Q2: any failure (timeout, bad JSON) becomes {"risk_score":0,"verdict":"ERROR",...}."""
+    from chronos.sensor.client import BrainClient, ClientConfig
+
+    s = Server(FakeBackend(mode, delay=3.0))
+    try:
+        v = BrainClient(ClientConfig(url=f"{s.url}/api/generate", timeout=1.0)).analyze(["[EXEC] bash -> nc"])
+        assert v["verdict"] == "ERROR" and v["risk_score"] == 0 and v["reason"]
+    finally:
+        s.close()
+
+
+@pytest.fixture(scope="module")
+def tiny_service():
+    from chronos.brain.api.service import EngineService
+    from chronos.brain.engine.engine import EngineConfig
+
+    svc = EngineService.from_config(EngineConfig(model="tiny", device="cpu", max_slots=4, max_model_len=384,
+                                                 use_graphs=False, decode_burst=4))
+    s = Server(svc)
+    yield s
+    s.close()
+    svc.close()
+
+
+def test_real_engine_behind_api(tiny_service):
+    from chronos.sensor.client import BrainClient, ClientConfig, schema_format
+
+    url = f"{tiny_service.url}/api/generate"
+    v = BrainClient(ClientConfig(url=url, fmt=schema_format(), options={"num_predict": 40})).analyze(
+        ["[OPEN] attack_chain.sh -> /tmp/malware.bin", "[EXEC] attack_chain.sh -> curl"])
+    assert set(v) == {"risk_score", "verdict", "reason"}
+    body = requests.post(url, json={"prompt": "hi", "format": "json", "stream": False,
+                                    "options": {"num_predict": 16}}, timeout=60).json()
+    assert isinstance(json.loads(body["response"]), dict) and body["eval_count"] <= 16
+    r = requests.post(url, json={"prompt": "hi", "format": "json", "options": {"num_predict": 16}}, stream=True,
+                      timeout=60)
+    lines = [json.loads(l) for l in r.iter_lines() if l]
+    assert lines[-1]["done"] and isinstance(json.loads("".join(l["response"] for l in lines)), dict)
+
+
+def test_dp_router_two_replicas():
+    from chronos.brain.api.protocol import GenerateParams
+    from chronos.brain.engine.engine import EngineConfig
+    from chronos.parallel.router import DPRouter
+    from chronos.sensor.prompt import VERDICT_SCHEMA
+
+    router = DPRouter(EngineConfig(model="tiny", device="cpu", max_slots=4, max_model_len=384, use_graphs=False,
+                                   decode_burst=4), 2)
+    try:
+        async def go():
+            ps = [GenerateParams(prompt=f"chain {i}", stream=False, format=VERDICT_SCHEMA, num_predict=32)
+                  for i in range(6)]
+            return await asyncio.gather(*[router.generate(p) for p in ps])
+
+        out = asyncio.run(go())
+        assert {o.rank for o in out} == {0, 1}
+        for o in out:
+            assert set(json.loads(o.text)) == {"risk_score", "verdict", "reason"}
+    finally:
+        router.close()
