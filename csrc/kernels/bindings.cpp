@@ -25,6 +25,7 @@ void launch_paged_attn(const uint16_t*, const uint16_t*, const uint16_t*, const 
 void launch_constrained_sample(const void*, bool, int64_t, const int32_t*, int, int, const int16_t*, const int16_t*,
                                int, int32_t*, int32_t*, const float*, const int32_t*, int32_t*, int32_t*, int32_t*,
                                int32_t*, int32_t*, int, hipStream_t);
+void launch_gemv(const uint16_t*, int, int, const uint16_t*, int, uint16_t*, bool, hipStream_t);
 }  // namespace chronos
 
 namespace {
@@ -208,6 +209,21 @@ void constrained_sample(const Tensor& logits, const c10::optional<Tensor>& row_o
                                        i32m(ctx), i32m(nout), i32m(out_tokens), (int)out_tokens.size(1), cur_stream());
 }
 
+// y = x @ w.T for M <= 8 rows (decode); swiglu: w = [gate; up] -> y = silu(x@gate.T) * (x@up.T)
+Tensor gemv(const Tensor& x, const Tensor& w, bool swiglu) {
+    chk_bf16(x, "x");
+    chk_bf16(w, "w");
+    const int64_t K = x.size(-1), M = x.numel() / K, N = w.size(0);
+    CHK(w.dim() == 2 && w.size(1) == K, "gemv: w must be [N, K]");
+    CHK(M >= 1 && M <= 8, "gemv: 1 <= M <= 8");
+    CHK(K % 512 == 0, "gemv: K % 512 == 0");
+    CHK(N % 16 == 0, "gemv: N % 16 == 0");
+    c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+    auto y = at::empty({M, swiglu ? N / 2 : N}, x.options());
+    chronos::launch_gemv(bf(x), (int)M, (int)K, bf(w), (int)N, bfm(y), swiglu, cur_stream());
+    return y;
+}
+
 }  // namespace
 
 TORCH_LIBRARY(chronos, m) {
@@ -217,6 +233,7 @@ TORCH_LIBRARY(chronos, m) {
     m.def("rope_kv_write(Tensor qkv, Tensor pos, Tensor tok_seq, Tensor block_table, Tensor cos_sin, "
           "Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, int hq, int hkv, bool write_q) -> ()");
     m.def("silu_mul(Tensor gate_up) -> Tensor");
+    m.def("gemv(Tensor x, Tensor w, bool swiglu) -> Tensor");
     m.def("paged_attention(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_table, Tensor q_start, "
           "Tensor ctx_len, Tensor? tiles, int ntiles, int nqt, int nsplit, float scale) -> Tensor");
     m.def("constrained_sample(Tensor logits, Tensor? row_of_slot, Tensor next, Tensor dist, int done_state, "
@@ -230,6 +247,7 @@ TORCH_LIBRARY_IMPL(chronos, CUDA, m) {
     m.impl("add_rmsnorm", &add_rmsnorm);
     m.impl("rope_kv_write", &rope_kv_write);
     m.impl("silu_mul", &silu_mul);
+    m.impl("gemv", &gemv);
     m.impl("paged_attention", &paged_attention);
     m.impl("constrained_sample", &constrained_sample);
 }

@@ -458,7 +458,7 @@ class LlamaModel:
                                        sb.ntiles, sb.nqt, sb.nsplit, self.scale)
             o = tp.all_reduce(ops.linear(attn.view(T, -1), lw.wo))
             x = ops.add_rmsnorm(o, resid, lw.mlp_norm, eps)
-            a = ops.silu_mul(ops.linear(x, lw.w_gu))
+            a = ops.gate_up_silu(x, lw.w_gu)
             dn = tp.all_reduce(ops.linear(a, lw.w_down))
             if li + 1 < len(w.layers):
                 x = ops.add_rmsnorm(dn, resid, w.layers[li + 1].attn_norm, eps)

@@ -13,7 +13,7 @@ import math
 import torch
 
 from . import reference as ref
-from .gemm import linear  # noqa: F401  (re-export)
+from .gemm import gate_up_silu, linear  # noqa: F401  (re-export)
 
 _loaded = False
 

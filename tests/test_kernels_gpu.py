@@ -249,3 +249,31 @@ def test_engine_graph_equals_eager():
             v = json.loads(r.text)
             assert {"risk_score", "verdict", "reason"} <= set(v)
     assert outs[0] == outs[1]
+
+
+@pytest.mark.parametrize("m", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("n,k", [(6144, 4096), (4096, 14336), (1024, 512), (48, 2560)])
+def test_gemv_matches_matmul(m, n, k):
+    from chronos.ops import gemm
+
+    g = torch.Generator(device=DEV).manual_seed(m * n + k)
+    x = torch.randn(m, k, device=DEV, generator=g).to(torch.bfloat16)
+    w = (torch.randn(n, k, device=DEV, generator=g) * 0.02).to(torch.bfloat16)
+    y = gemm._gemv(x, w)
+    ref = (x.float() @ w.float().t())
+    _close(y, ref, 2e-2, 2e-2)
+
+
+@pytest.mark.parametrize("m", [1, 2, 4, 7, 8])
+def test_gemv_fused_swiglu(m):
+    from chronos import ops
+    from chronos.ops import gemm
+    from chronos.ops import reference as ref
+
+    g = torch.Generator(device=DEV).manual_seed(m)
+    x = torch.randn(m, 4096, device=DEV, generator=g).to(torch.bfloat16)
+    w = (torch.randn(2 * 1792, 4096, device=DEV, generator=g) * 0.02).to(torch.bfloat16)
+    y = gemm._gemv(x, w, True)
+    exp = ref.silu_mul((x.float() @ w.float().t()).to(torch.bfloat16))
+    _close(y, exp, 2e-2, 3e-2)
+    assert ops.gate_up_silu(x, w).shape == (m, 1792)
