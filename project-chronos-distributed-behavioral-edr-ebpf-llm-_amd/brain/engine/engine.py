@@ -126,6 +126,12 @@ class Engine:
                 nb = max(2, min(nb, need))
             else:
                 nb = need
+        if self.tp.world > 1:  # lockstep TP scheduling needs the same block budget on every rank
+            import torch.distributed as dist
+
+            t = torch.tensor([nb], dtype=torch.int64, device=self.device)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.tp.group)
+            nb = int(t.item())
         self.kv = KVCache(mc, self.tp, nb, bs, self.device)
         self.blocks = BlockManager(nb, bs)
         # ---- slot state (device) ----

@@ -1,0 +1,117 @@
+"""Tensor-parallel Brain replica (Llama-3-70B TP=8 over xGMI; SURVEY.md §2.5 TP, §2.4 C1-C5).
+
+One process per GPU of the TP group.  Every rank runs the SAME Engine (its weight shards, its KV-head shard) and the
+SAME scheduler, in lockstep:
+
+* the leader (TP rank 0) owns the request queue; once per step it broadcasts the requests that arrived since the
+  previous step (C5 — a few hundred bytes over a host-side gloo group, never through the GPU stream);
+* every rank submits them in the same order, so admission, KV block allocation, slot assignment and prefill packing
+  are identical by construction;
+* logits are all-gathered (vocab-parallel LM head), so the fused constrained sampler computes the same tokens and
+  advances the same device state on every rank — no token broadcast, and the decode burst stays one captured graph
+  per rank with the RCCL all-reduces inside it;
+* finished requests are reported by the leader; followers just retire them.
+"""
+from __future__ import annotations
+
+import queue
+import threading
+from dataclasses import dataclass, field
+from typing import Any, Callable, Optional
+
+import torch.distributed as dist
+
+from ..brain.engine.engine import Engine, EngineConfig, Request
+from .tp import TPContext
+
+
+@dataclass
+class _Sub:
+    ids: list
+    fmt: Any = None
+    num_predict: Optional[int] = None
+    temperature: float = 0.0
+    seed: int = 0
+    tag: int = 0
+
+
+@dataclass
+class _Msg:
+    subs: list = field(default_factory=list)
+    stop: bool = False
+
+
+class TPEngine:
+    def __init__(self, cfg: EngineConfig, tp: TPContext, ctrl_group=None):
+        self.tp = tp
+        self.ctrl = ctrl_group  # gloo group spanning the TP ranks (host-side control plane)
+        self.engine = Engine(cfg, tp=tp)
+        self.leader = tp.rank == 0
+        self._inbox: "queue.Queue[_Sub]" = queue.Queue()
+        self._callbacks: dict[int, Callable[[Request], None]] = {}
+        self._tag = 0
+        self._lock = threading.Lock()
+
+    # ---- leader API ----------------------------------------------------------------------------------------------
+    def submit(self, prompt, fmt=None, num_predict: int | None = None, temperature: float = 0.0, seed: int = 0,
+               callback: Callable[[Request], None] | None = None) -> int:
+        assert self.leader, "requests enter through TP rank 0"
+        ids = prompt if isinstance(prompt, list) else self.engine.tok.chat_ids(prompt)
+        with self._lock:
+            self._tag += 1
+            tag = self._tag
+            if callback is not None:
+                self._callbacks[tag] = callback
+        self._inbox.put(_Sub(ids, fmt, num_predict, temperature, seed, tag))
+        return tag
+
+    def _exchange(self, stop: bool = False) -> _Msg:
+        msg = _Msg()
+        if self.leader:
+            while True:
+                try:
+                    msg.subs.append(self._inbox.get_nowait())
+                except queue.Empty:
+                    break
+            msg.stop = stop
+        if self.tp.world > 1:
+            box = [msg]
+            dist.broadcast_object_list(box, src=dist.get_global_rank(self.ctrl, 0) if self.ctrl else 0,
+                                       group=self.ctrl)
+            msg = box[0]
+        return msg
+
+    def step(self, stop: bool = False) -> tuple[list[Request], bool]:
+        """One lockstep iteration on every rank.  Returns (finished requests, stop flag)."""
+        msg = self._exchange(stop)
+        for s in msg.subs:
+            cb = self._callbacks.pop(s.tag, None) if self.leader else None
+            self.engine.submit(s.ids, fmt=s.fmt, num_predict=s.num_predict, temperature=s.temperature, seed=s.seed,
+                               callback=cb, meta={"tag": s.tag})
+        done = self.engine.step() if self.engine.has_work() else []
+        return done, msg.stop
+
+    def run_until_idle(self) -> list[Request]:
+        """Leader: drive all ranks until every submitted request finished, then tell followers to stop serving."""
+        out = []
+        while True:
+            pending = self.engine.has_work() or not self._inbox.empty()
+            done, _ = self.step(stop=not pending)
+            out += done
+            if not pending:
+                return out
+
+    def follower_loop(self) -> None:
+        while True:
+            _, stop = self.step()
+            if stop and not self.engine.has_work():
+                return
+
+
+def init_tp(backend: str = "nccl") -> tuple[TPContext, Any]:
+    """Initialise the default process group (env:// rendezvous) + a gloo control group over the same ranks."""
+    if not dist.is_initialized():
+        dist.init_process_group(backend)
+    tp = TPContext.from_group()
+    ctrl = dist.new_group(backend="gloo") if backend != "gloo" else None
+    return tp, ctrl

@@ -26,6 +26,19 @@ for r in rows:
     if cur is not None:
         cur["kernels"].append(r)
 dur = lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3  # noqa: E731
+# device idle: gaps between consecutive kernels (host-side scheduling / sync / python overhead)
+span = (int(rows[-1]["End_Timestamp"]) - int(rows[0]["Start_Timestamp"])) / 1e3
+busy = sum(dur(r) for r in rows)
+gaps = []
+for a, b in zip(rows, rows[1:]):
+    g = (int(b["Start_Timestamp"]) - int(a["End_Timestamp"])) / 1e3
+    if g > 0:
+        gaps.append((g, a["Kernel_Name"][:50], b["Kernel_Name"][:50]))
+big = [g for g in gaps if g[0] > 50]
+print(f"trace span {span/1e3:.1f} ms, kernel busy {busy/1e3:.1f} ms ({100*busy/span:.1f}%), "
+      f"gaps>50us: {len(big)} totalling {sum(g[0] for g in big)/1e3:.1f} ms")
+for g in sorted(big, reverse=True)[:8]:
+    print(f"   gap {g[0]/1e3:8.2f} ms after {g[1]} -> {g[2]}")
 byT = collections.defaultdict(list)
 for f in fw:
     byT[f["T"]].append(f)
