@@ -26,6 +26,8 @@ void launch_constrained_sample(const void*, bool, int64_t, const int32_t*, int, 
                                int, int32_t*, int32_t*, const float*, const int32_t*, int32_t*, int32_t*, int32_t*,
                                int32_t*, int32_t*, int, hipStream_t);
 void launch_gemv(const uint16_t*, int, int, const uint16_t*, int, uint16_t*, bool, hipStream_t);
+void launch_attn_prefill(const uint16_t*, const uint16_t*, const uint16_t*, const int32_t*, int, const int32_t*,
+                         const int32_t*, const int32_t*, int, uint16_t*, int, int, int, float, hipStream_t);
 }  // namespace chronos
 
 namespace {
@@ -140,7 +142,7 @@ Tensor paged_attention(const Tensor& q, const Tensor& k_cache, const Tensor& v_c
     CHK(hq % hkv == 0 && 16 % (hq / hkv) == 0, "GQA group Hq/Hkv must divide 16");
     CHK(bs % 16 == 0, "block size must be a multiple of 16");
     CHK(v_cache.size(2) == 128 && v_cache.size(3) == bs, "v_cache [NB, hkv, 128, BS]");
-    CHK(nqt == 1 || nqt == 2, "nqt must be 1 or 2");
+    CHK(nqt == 1 || nqt == 2 || nqt == 8, "nqt must be 1, 2 (split-K paged kernel) or 8 (flash prefill)");
     CHK(nsplit >= 1 && nsplit <= 256, "nsplit in [1, 256]");
     const int32_t* tp = nullptr;
     if (tiles.has_value()) {
@@ -153,10 +155,17 @@ Tensor paged_attention(const Tensor& q, const Tensor& k_cache, const Tensor& v_c
     c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
     auto out = at::empty_like(q);
     Tensor po, pl;
-    if (nsplit > 1) {
+    if (nsplit > 1 && nqt != 8) {
         const int64_t rows = nsplit * ntiles * hkv * nqt * 16;
         po = at::empty({rows, 128}, q.options().dtype(at::kFloat));
         pl = at::empty({rows}, q.options().dtype(at::kFloat));
+    }
+    if (nqt == 8) {  // flash prefill kernel: 128 query rows per workgroup, K/V tiles shared through LDS
+        CHK(tp != nullptr, "nqt=8 (flash prefill) needs a tile list");
+        chronos::launch_attn_prefill(bf(q), bf(k_cache), bf(v_cache), i32(block_table), (int)block_table.size(1),
+                                     i32(q_start), i32(ctx_len), tp, (int)ntiles, bfm(out), (int)hq, (int)hkv,
+                                     (int)bs, (float)scale, cur_stream());
+        return out;
     }
     chronos::launch_paged_attn(bf(q), bf(k_cache), bf(v_cache), i32(block_table), (int)block_table.size(1),
                                i32(q_start), i32(ctx_len), tp, (int)ntiles, (int)nqt, (int)nsplit, bfm(out),

@@ -58,7 +58,7 @@ class EngineConfig:
     use_graphs: bool = True
     grammar_capacity: int = 2048
     max_string: int = 160          # default maxLength for schema strings without one (keeps verdicts short)
-    prefill_nqt: int = 2
+    prefill_nqt: int = 8           # 8 = flash prefill kernel (128 query rows / workgroup); 1-2 = split-K kernel
 
 
 @dataclass

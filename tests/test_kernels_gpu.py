@@ -114,8 +114,8 @@ def _attn_case(q_lens, ctx_lens, hq, hkv, bs, seed):
         torch.tensor(ctx_lens, dtype=torch.int32, device=DEV)
 
 
-@pytest.mark.parametrize("nqt", [1, 2])
-@pytest.mark.parametrize("hq,hkv,bs", [(32, 8, 16), (16, 2, 16), (8, 1, 32)])
+@pytest.mark.parametrize("nqt", [1, 2, 8])
+@pytest.mark.parametrize("hq,hkv,bs", [(32, 8, 16), (16, 2, 16), (8, 1, 32), (4, 4, 16)])
 @pytest.mark.parametrize("nsplit", [1, 3])
 def test_paged_attention_prefill(nqt, hq, hkv, bs, nsplit):
     from chronos import ops
@@ -128,6 +128,20 @@ def test_paged_attention_prefill(nqt, hq, hkv, bs, nsplit):
     tt = torch.tensor(tiles, dtype=torch.int32, device=DEV).view(-1, 2)
     out = ops.paged_attention(q, k, v, bt, qs, ctx, tt, len(tiles), nqt, nsplit)
     exp = ref.paged_attention(q, k, v, bt, qs, ctx, tt, len(tiles), nqt, nsplit)
+    _close(out, exp, 2e-2, 2e-2)
+
+
+def test_flash_prefill_long_prefix():
+    """Chunked prefill of 300 tokens on a 1700-token cached prefix + a fresh 513-token prompt (flash kernel)."""
+    from chronos import ops
+    from chronos.ops import reference as ref
+
+    q_lens, ctx_lens = [300, 513], [2000, 513]
+    q, k, v, bt, qs, ctx = _attn_case(q_lens, ctx_lens, 32, 8, 16, seed=77)
+    tiles = ops.attention_tiles(q_lens, 32, 8, 8)
+    tt = torch.tensor(tiles, dtype=torch.int32, device=DEV).view(-1, 2)
+    out = ops.paged_attention(q, k, v, bt, qs, ctx, tt, len(tiles), 8, 1)
+    exp = ref.paged_attention(q, k, v, bt, qs, ctx, tt, len(tiles), 8, 1)
     _close(out, exp, 2e-2, 2e-2)
 
 
