@@ -33,7 +33,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=4)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--model", default="llama3-8b")
-    ap.add_argument("--streams", type=int, default=512, help="concurrent sensor streams (chains per step) per GPU")
+    ap.add_argument("--streams", type=int, default=1024, help="concurrent sensor streams (chains per step) per GPU")
     ap.add_argument("--num-predict", type=int, default=64)
     ap.add_argument("--single-stream", type=int, default=8, help="chains for the single-stream p50 latency")
     ap.add_argument("--burst", type=int, default=8)

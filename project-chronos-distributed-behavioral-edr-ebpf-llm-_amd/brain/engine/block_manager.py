@@ -1,37 +1,112 @@
-"""Paged-KV block allocator.
+"""Paged-KV block allocator with automatic prefix caching (SURVEY.md §1.2 N4, §5.7 "prefix caching of the fixed
+prompt template").
+
+Every CHRONOS prompt starts with the same Llama-3 chat header + "Analyze this sequence. Return JSON ONLY.\\n
+Sequence: [" (chronos_sensor.py:109-111): one full 16-token KV block that every chain would otherwise recompute.
+Full blocks of prompt tokens are content-addressed by a chained hash (parent hash, token ids); a new request reuses
+the longest cached run of its prompt's full blocks (refcounted, read-only) and prefills only the remainder.  Blocks
+whose refcount drops to zero stay cached and are recycled least-recently-used when the free list runs dry.
 
 Block 0 is reserved as a scratch block: empty decode slots point their block table at it, so a captured decode graph
 that always runs a fixed number of rows never writes into another sequence's KV.
 """
 from __future__ import annotations
 
+from collections import OrderedDict
+from typing import Sequence
+
 
 class BlockManager:
-    def __init__(self, num_blocks: int, block_size: int):
+    def __init__(self, num_blocks: int, block_size: int, prefix_cache: bool = True):
         if num_blocks < 2:
             raise ValueError("need at least 2 KV blocks (block 0 is scratch)")
         self.num_blocks, self.block_size = num_blocks, block_size
+        self.prefix_cache = prefix_cache
         self._free = list(range(num_blocks - 1, 0, -1))
+        self._ref: dict[int, int] = {}
+        self._by_hash: dict[int, int] = {}       # content hash -> block
+        self._hash_of: dict[int, int] = {}       # block -> content hash
+        self._evictable: "OrderedDict[int, None]" = OrderedDict()  # cached blocks with refcount 0 (LRU order)
+        self.hits = 0
+        self.lookups = 0
 
     def blocks_for(self, tokens: int) -> int:
         return (tokens + self.block_size - 1) // self.block_size
 
     @property
     def free(self) -> int:
-        return len(self._free)
+        return len(self._free) + len(self._evictable)
 
     def can_alloc(self, n: int) -> bool:
-        return len(self._free) >= n
+        return self.free >= n
+
+    def _take(self) -> int:
+        if self._free:
+            return self._free.pop()
+        b, _ = self._evictable.popitem(last=False)  # least recently used cached block
+        h = self._hash_of.pop(b)
+        self._by_hash.pop(h, None)
+        return b
 
     def alloc(self, n: int) -> list[int]:
-        if n > len(self._free):
-            raise MemoryError(f"KV cache exhausted: want {n} blocks, {len(self._free)} free")
-        out = self._free[-n:][::-1] if n else []
-        del self._free[len(self._free) - n:]
+        if n > self.free:
+            raise MemoryError(f"KV cache exhausted: want {n} blocks, {self.free} free")
+        out = [self._take() for _ in range(n)]
+        for b in out:
+            self._ref[b] = 1
         return out
 
-    def release(self, blocks: list[int]) -> None:
-        self._free.extend(reversed(blocks))
+    def release(self, blocks: Sequence[int]) -> None:
+        for b in blocks:
+            r = self._ref.get(b, 0) - 1
+            if r > 0:
+                self._ref[b] = r
+                continue
+            self._ref.pop(b, None)
+            if b in self._hash_of:
+                self._evictable[b] = None
+            else:
+                self._free.append(b)
+
+    # ---- prefix cache ----------------------------------------------------------------------------------------------
+    def _hashes(self, tokens: Sequence[int], nblocks: int) -> list[int]:
+        hs, h = [], 0
+        bs = self.block_size
+        for i in range(nblocks):
+            h = hash((h, tuple(tokens[i * bs:(i + 1) * bs])))
+            hs.append(h)
+        return hs
+
+    def lookup(self, tokens: Sequence[int]) -> list[int]:
+        """Longest run of cached full blocks at the start of `tokens` (never the whole prompt: the last token must be
+        recomputed for its logits).  The returned blocks are referenced for the caller."""
+        if not self.prefix_cache:
+            return []
+        self.lookups += 1
+        n = (len(tokens) - 1) // self.block_size
+        out = []
+        for h in self._hashes(tokens, n):
+            b = self._by_hash.get(h)
+            if b is None:
+                break
+            out.append(b)
+        for b in out:
+            if b in self._evictable:
+                del self._evictable[b]
+            self._ref[b] = self._ref.get(b, 0) + 1
+        self.hits += bool(out)
+        return out
+
+    def register(self, tokens: Sequence[int], blocks: Sequence[int]) -> None:
+        """After a prompt's KV is written: publish its full blocks for reuse."""
+        if not self.prefix_cache:
+            return
+        n = min(len(tokens) // self.block_size, len(blocks))
+        for h, b in zip(self._hashes(tokens, n), blocks[:n]):
+            if h in self._by_hash or b in self._hash_of:
+                continue
+            self._by_hash[h] = b
+            self._hash_of[b] = h
 
     def usage(self) -> float:
-        return 1.0 - len(self._free) / (self.num_blocks - 1)
+        return 1.0 - self.free / (self.num_blocks - 1)

@@ -1,0 +1,60 @@
+"""Prefix caching: reusing the shared CHRONOS template block changes nothing but the work done."""
+import pytest
+
+from chronos.brain.engine.block_manager import BlockManager
+
+
+def test_block_manager_refcounts_and_lru():
+    bm = BlockManager(10, 4)
+    toks = list(range(13))           # 3 full blocks + 1 token
+    a = bm.alloc(4)
+    bm.register(toks, a)
+    assert bm.lookup(toks) == a[:3]  # never the block holding the last prompt token
+    bm.release(a)                    # owner done; the 3 shared still referenced by the lookup
+    assert bm.free == 9 - 3
+    bm.release(a[:3])                # sharer done: cached blocks become evictable, still hit
+    assert bm.free == 9 and bm.lookup(toks) == a[:3]
+    bm.release(a[:3])
+    taken = bm.alloc(9)              # pressure evicts the cached blocks (LRU) and forgets their hashes
+    assert len(set(taken)) == 9 and bm.lookup(toks) == []
+
+
+@pytest.mark.parametrize("chunk", [200, 40])
+def test_engine_prefix_cache_same_outputs(chunk):
+    from chronos.brain.engine.engine import Engine, EngineConfig
+    from chronos.sensor.prompt import VERDICT_SCHEMA, build_prompt
+    from chronos.sensor.replay import synthetic_chains
+
+    chains = synthetic_chains(10, seed=4, native=False)
+    outs, stats = [], []
+    for pc in (False, True):
+        eng = Engine(EngineConfig(model="tiny", device="cpu", max_slots=8, max_model_len=384, use_graphs=False,
+                                  prefix_cache=pc, max_prefill_tokens=chunk))
+        reqs = [eng.submit(build_prompt(c.history), fmt=VERDICT_SCHEMA, num_predict=30) for c in chains]
+        eng.run_until_idle()
+        outs.append([r.out_ids for r in reqs])
+        stats.append(dict(eng.stats))
+    assert outs[0] == outs[1]
+    assert stats[1]["prefix_hit_tokens"] >= 16 * 9 and stats[1]["prefill_tokens"] < stats[0]["prefill_tokens"]
+
+
+def test_slot_compaction_preserves_outputs():
+    """Verdicts of different lengths finish at different steps; compaction moves live rows down so the decode bucket
+    shrinks — every sequence must still produce exactly what it produces alone."""
+    from chronos.brain.engine.engine import Engine, EngineConfig
+    from chronos.sensor.prompt import VERDICT_SCHEMA, build_prompt
+    from chronos.sensor.replay import synthetic_chains
+
+    chains = synthetic_chains(12, seed=4, native=False)
+    budgets = list(range(16, 40, 2))
+    mk = lambda: Engine(EngineConfig(model="tiny", device="cpu", max_slots=16, max_model_len=384,  # noqa: E731
+                                     use_graphs=False, decode_burst=4))
+    eng = mk()
+    reqs = [eng.submit(build_prompt(c.history), fmt=VERDICT_SCHEMA, num_predict=n) for c, n in zip(chains, budgets)]
+    eng.run_until_idle()
+    assert eng.stats["compactions"] >= 1
+    solo_eng = mk()
+    for c, n, r in zip(chains, budgets, reqs):
+        s = solo_eng.submit(build_prompt(c.history), fmt=VERDICT_SCHEMA, num_predict=n)
+        solo_eng.run_until_idle()
+        assert s.out_ids == r.out_ids
