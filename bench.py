@@ -38,6 +38,7 @@ def parse():
     ap.add_argument("--single-stream", type=int, default=8, help="chains for the single-stream p50 latency")
     ap.add_argument("--burst", type=int, default=8)
     ap.add_argument("--no-graphs", action="store_true")
+    ap.add_argument("--no-prefix-cache", action="store_true")
     ap.add_argument("--device", default="cuda")
     return ap.parse_args()
 
@@ -60,13 +61,16 @@ def main():
 
     cfg = EngineConfig(model=a.model, device=str(device), max_slots=a.streams, max_model_len=512,
                        default_num_predict=a.num_predict, decode_burst=a.burst, use_graphs=not a.no_graphs,
-                       seed=0)
+                       prefix_cache=not a.no_prefix_cache, seed=0)
     eng = Engine(cfg)
     total_steps = a.warmup + a.steps
     chains = synthetic_chains(a.streams * total_steps + a.single_stream, seed=1000 + rank)
     prompts = [build_prompt(c.history) for c in chains]
 
     def run_step(batch):
+        # Nothing computed outside a step is reused inside it: the prefix cache starts empty every step, so only
+        # chains arriving in the same wave share identical prompt-prefix KV blocks (computed once, in this step).
+        eng.blocks.clear_cache()
         reqs = [eng.submit(p, fmt=VERDICT_SCHEMA, num_predict=a.num_predict) for p in batch]
         eng.run_until_idle()
         return reqs
@@ -87,6 +91,7 @@ def main():
         run_step(prompts[s * a.streams:(s + 1) * a.streams])
         progress(f"warmup step {s}: {time.perf_counter() - t:.2f}s {dict(eng.stats)}")
     barrier()
+    hit0 = eng.stats["prefix_hit_tokens"]
     t0 = time.perf_counter()
     timed = []
     for s in range(a.warmup, total_steps):
@@ -94,6 +99,7 @@ def main():
         progress(f"step {s} done")
     barrier()
     elapsed = time.perf_counter() - t0
+    hits = eng.stats["prefix_hit_tokens"] - hit0
 
     ok = 0
     for r in timed:
@@ -112,7 +118,8 @@ def main():
         single += run_step([p])
     single_lat = [r.latency for r in single[1:]] or [r.latency for r in single]
 
-    stats = dict(elapsed=elapsed, ok=ok, n=len(timed), lat=lat, gen=gen_tok, ptok=prompt_tok, single=single_lat)
+    stats = dict(elapsed=elapsed, ok=ok, n=len(timed), lat=lat, gen=gen_tok, ptok=prompt_tok, single=single_lat,
+                 hits=hits)
     if world > 1:
         allst = [None] * world
         dist.all_gather_object(allst, stats)
@@ -151,6 +158,7 @@ def main():
             "prompt_tokens_per_chain": round(sum(s["ptok"] for s in allst) / n, 1),
             "verdict_tokens_per_chain": round(sum(s["gen"] for s in allst) / n, 1),
             "generated_tokens_per_s": round(sum(s["gen"] for s in allst) / t, 1),
+            "prefix_cache_hit_fraction": round(sum(s["hits"] for s in allst) / max(1, sum(s["ptok"] for s in allst)), 3),
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -108,5 +108,13 @@ class BlockManager:
             self._by_hash[h] = b
             self._hash_of[b] = h
 
+    def clear_cache(self) -> None:
+        """Forget every cached prefix (blocks still referenced keep their contents; idle cached blocks are freed)."""
+        for b in list(self._evictable):
+            self._free.append(b)
+        self._evictable.clear()
+        self._by_hash.clear()
+        self._hash_of.clear()
+
     def usage(self) -> float:
         return 1.0 - self.free / (self.num_blocks - 1)

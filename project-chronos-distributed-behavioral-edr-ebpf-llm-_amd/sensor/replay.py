@@ -119,9 +119,11 @@ class SyntheticTelemetry:
         return self.next_pid
 
     def _file(self, user: str) -> str:
+        # a random 24-bit hex tag per file: fleet telemetry rarely repeats exact paths, and a low-entropy generator
+        # would make the Brain's prefix cache look better than it is on real chains
         r = self.rng
         d = r.choice([f"/home/{user}", f"/home/{user}/src", "/tmp", "/var/tmp", "/opt/app", f"/home/{user}/Downloads"])
-        return f"{d}/{r.choice(_WORDS)}{r.randint(0, 99)}{r.choice(_EXTS)}"
+        return f"{d}/{r.choice(_WORDS)}_{r.getrandbits(24):06x}{r.choice(_EXTS)}"
 
     def _noise(self, pid: int, comm: str) -> list[bytes]:
         r = self.rng
@@ -164,7 +166,7 @@ class SyntheticTelemetry:
         parent = r.choice(["bash", "sh", "update.sh", "attack_chain.sh", "cron", "apache2"])
         kind = r.randrange(5)
         out: list[bytes] = []
-        drop = f"/tmp/{r.choice(_WORDS)}{r.randint(0, 999)}{r.choice(['.bin', '', '.sh', '.elf'])}"
+        drop = f"/tmp/{r.choice(_WORDS)}{r.getrandbits(20):05x}{r.choice(['.bin', '', '.sh', '.elf'])}"
         if kind == 0:      # T1105 ingress tool transfer + execution
             p1, p2, p3 = self._pid(), self._pid(), self._pid()
             tool = r.choice(["curl", "wget"])
