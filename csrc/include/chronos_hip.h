@@ -53,6 +53,28 @@ __device__ __forceinline__ float block_sum(float v, float* red) {
     return r;
 }
 
+// ---- fp8 e4m3 (OCP "fn" encoding on gfx950 — not MI300's fnuz) KV-cache helpers ---------------------------------
+constexpr float kFp8Max = 448.f;
+__device__ __forceinline__ uint32_t f32x4_to_fp8x4(float a, float b, float c, float d) {
+    a = fminf(fmaxf(a, -kFp8Max), kFp8Max);  // e4m3fn has no infinity: saturate instead of producing NaN
+    b = fminf(fmaxf(b, -kFp8Max), kFp8Max);
+    c = fminf(fmaxf(c, -kFp8Max), kFp8Max);
+    d = fminf(fmaxf(d, -kFp8Max), kFp8Max);
+    int r = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+    r = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, r, true);
+    return (uint32_t)r;
+}
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ bf16x4 fp8x4_to_bf16x4(uint32_t v, float scale) {
+    const f32x2_t lo = __builtin_amdgcn_cvt_pk_f32_fp8((int)v, false);
+    const f32x2_t hi = __builtin_amdgcn_cvt_pk_f32_fp8((int)v, true);
+    return bf16x4{(__bf16)(lo[0] * scale), (__bf16)(lo[1] * scale), (__bf16)(hi[0] * scale), (__bf16)(hi[1] * scale)};
+}
+__device__ __forceinline__ bf16x8 fp8x8_to_bf16x8(uint32_t v0, uint32_t v1, float scale) {
+    const bf16x4 a = fp8x4_to_bf16x4(v0, scale), b = fp8x4_to_bf16x4(v1, scale);
+    return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
 // XCD-aware bijective block remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective"): consecutive logical
 // tiles land on the same XCD (shared L2).  Speed only; correctness never depends on placement.
 __device__ __forceinline__ int xcd_remap(int orig, int nwg) {

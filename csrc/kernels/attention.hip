@@ -26,13 +26,18 @@ namespace chronos {
 constexpr int kD = 128;
 constexpr int kOStride = 132;  // LDS row stride (floats) of the merge buffer: breaks the 512-B row bank aliasing
 
-template <int NQT>
+template <int NQT, bool FP8>
 __global__ void __launch_bounds__(256) paged_attn_kernel(
-    const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
+    const uint16_t* __restrict__ q, const void* __restrict__ kcv, const void* __restrict__ vcv,
     const int32_t* __restrict__ block_table, int bt_stride, const int32_t* __restrict__ q_start,
     const int32_t* __restrict__ ctx_len, const int32_t* __restrict__ tiles, uint16_t* __restrict__ out,
-    float* __restrict__ part_o, float* __restrict__ part_lse, int hq, int hkv, int block_size, float scale_log2) {
+    float* __restrict__ part_o, float* __restrict__ part_lse, int hq, int hkv, int block_size, float scale_log2,
+    float k_scale, float v_scale) {
     constexpr int ROWS = NQT * 16;
+    const uint16_t* kc = reinterpret_cast<const uint16_t*>(kcv);
+    const uint16_t* vc = reinterpret_cast<const uint16_t*>(vcv);
+    const uint8_t* kc8 = reinterpret_cast<const uint8_t*>(kcv);
+    const uint8_t* vc8 = reinterpret_cast<const uint8_t*>(vcv);
     extern __shared__ __attribute__((aligned(16))) float smem[];
     float* sm = smem;                 // [4][ROWS]
     float* sl = sm + 4 * ROWS;        // [4][ROWS]
@@ -104,13 +109,25 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
             if (tg < ke) {
                 const int64_t blk = bt[tg / block_size];
                 const int off = tg % block_size;
-                const uint16_t* kp = kc + (((blk * hkv + h) * block_size) + off + r) * kD + 8 * h4;
+                const int64_t koff = (((blk * hkv + h) * block_size) + off + r) * kD + 8 * h4;
+                const int64_t voff = ((blk * hkv + h) * kD) * (int64_t)block_size + off + 4 * h4;
+                if constexpr (FP8) {  // 1-byte e4m3 cache, dequantised to the bf16 MFMA operands in registers
 #pragma unroll
-                for (int c = 0; c < 4; ++c) kf[g][c] = *reinterpret_cast<const bf16x8*>(kp + 32 * c);
-                const uint16_t* vp = vc + ((blk * hkv + h) * kD) * (int64_t)block_size + off + 4 * h4;
+                    for (int c = 0; c < 4; ++c) {
+                        const uint2 v = *reinterpret_cast<const uint2*>(kc8 + koff + 32 * c);
+                        kf[g][c] = fp8x8_to_bf16x8(v.x, v.y, k_scale);
+                    }
 #pragma unroll
-                for (int dt = 0; dt < 8; ++dt)
-                    vf[g][dt] = *reinterpret_cast<const bf16x4*>(vp + (int64_t)(dt * 16 + r) * block_size);
+                    for (int dt = 0; dt < 8; ++dt)
+                        vf[g][dt] = fp8x4_to_bf16x4(
+                            *reinterpret_cast<const uint32_t*>(vc8 + voff + (int64_t)(dt * 16 + r) * block_size), v_scale);
+                } else {
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) kf[g][c] = *reinterpret_cast<const bf16x8*>(kc + koff + 32 * c);
+#pragma unroll
+                    for (int dt = 0; dt < 8; ++dt)
+                        vf[g][dt] = *reinterpret_cast<const bf16x4*>(vc + voff + (int64_t)(dt * 16 + r) * block_size);
+                }
             } else {
 #pragma unroll
                 for (int c = 0; c < 4; ++c) kf[g][c] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
@@ -268,29 +285,36 @@ __global__ void __launch_bounds__(256) paged_attn_combine_kernel(
 
 size_t paged_attn_smem(int nqt) { return (size_t)(8 * nqt * 16 + 4 * nqt * 16 * kOStride) * sizeof(float); }
 
-void launch_paged_attn(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* block_table,
-                       int bt_stride, const int32_t* q_start, const int32_t* ctx_len, const int32_t* tiles,
-                       int ntiles, int nqt, int nsplit, uint16_t* out, float* part_o, float* part_lse, int hq,
-                       int hkv, int block_size, float scale, hipStream_t st) {
+void launch_paged_attn(const uint16_t* q, const void* kc, const void* vc, const int32_t* block_table, int bt_stride,
+                       const int32_t* q_start, const int32_t* ctx_len, const int32_t* tiles, int ntiles, int nqt,
+                       int nsplit, uint16_t* out, float* part_o, float* part_lse, int hq, int hkv, int block_size,
+                       float scale, bool fp8, float k_scale, float v_scale, hipStream_t st) {
     if (ntiles == 0) return;
     const float scale_log2 = scale * 1.4426950408889634f;
     const dim3 grid(ntiles, hkv, nsplit), block(256);
     const size_t sh = paged_attn_smem(nqt);
+#define PA_LAUNCH(N, F)                                                                                         \
+    hipLaunchKernelGGL((paged_attn_kernel<N, F>), grid, block, sh, st, q, kc, vc, block_table, bt_stride, q_start, \
+                       ctx_len, tiles, out, part_o, part_lse, hq, hkv, block_size, scale_log2, k_scale, v_scale)
     if (nqt == 1) {
-        hipLaunchKernelGGL(paged_attn_kernel<1>, grid, block, sh, st, q, kc, vc, block_table, bt_stride, q_start,
-                           ctx_len, tiles, out, part_o, part_lse, hq, hkv, block_size, scale_log2);
-        if (nsplit > 1)
-            hipLaunchKernelGGL(paged_attn_combine_kernel<1>, dim3(ntiles, hkv), block, 0, st, part_o, part_lse,
-                               q_start, tiles, out, hq, hkv, nsplit, ntiles);
+        if (fp8) PA_LAUNCH(1, true); else PA_LAUNCH(1, false);
     } else {
         static bool attr = [] {  // > 64 KiB dynamic LDS needs the opt-in (gfx950 has 160 KiB per CU)
-            return hipFuncSetAttribute((const void*)paged_attn_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)paged_attn_smem(2)) == hipSuccess;
+            const int b = (int)paged_attn_smem(2);
+            return hipFuncSetAttribute((const void*)paged_attn_kernel<2, false>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, b) == hipSuccess &&
+                   hipFuncSetAttribute((const void*)paged_attn_kernel<2, true>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, b) == hipSuccess;
         }();
         (void)attr;
-        hipLaunchKernelGGL(paged_attn_kernel<2>, grid, block, sh, st, q, kc, vc, block_table, bt_stride, q_start,
-                           ctx_len, tiles, out, part_o, part_lse, hq, hkv, block_size, scale_log2);
-        if (nsplit > 1)
+        if (fp8) PA_LAUNCH(2, true); else PA_LAUNCH(2, false);
+    }
+#undef PA_LAUNCH
+    if (nsplit > 1) {
+        if (nqt == 1)
+            hipLaunchKernelGGL(paged_attn_combine_kernel<1>, dim3(ntiles, hkv), block, 0, st, part_o, part_lse,
+                               q_start, tiles, out, hq, hkv, nsplit, ntiles);
+        else
             hipLaunchKernelGGL(paged_attn_combine_kernel<2>, dim3(ntiles, hkv), block, 0, st, part_o, part_lse,
                                q_start, tiles, out, hq, hkv, nsplit, ntiles);
     }

@@ -22,12 +22,15 @@ constexpr int kVPitch = 80;     // V^T row pitch (bytes)
 constexpr int kVImg = 128 * kVPitch;
 constexpr int kStage = kKImg + kVImg;
 
+template <bool FP8>
 __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(
-    const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
+    const uint16_t* __restrict__ q, const void* __restrict__ kcv, const void* __restrict__ vcv,
     const int32_t* __restrict__ block_table, int bt_stride, const int32_t* __restrict__ q_start,
     const int32_t* __restrict__ ctx_len, const int32_t* __restrict__ tiles, int ntiles, uint16_t* __restrict__ out,
-    int hq, int hkv, int block_size, float scale_log2) {
+    int hq, int hkv, int block_size, float scale_log2, float k_scale, float v_scale) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const uint16_t* kc = reinterpret_cast<const uint16_t*>(kcv);
+    const uint16_t* vc = reinterpret_cast<const uint16_t*>(vcv);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int r = lane & 15, h4 = lane >> 4;
     const int G = hq / hkv;
@@ -70,18 +73,32 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(
         const int tok = s * 32 + krow;
         if (tok < kv_end) {
             const int64_t blk = bt[tok / block_size];
-            const u16x8* p = reinterpret_cast<const u16x8*>(kc + (((blk * hkv + h) * block_size) + tok % block_size) * kPD) + kunit;
-            ks[0] = p[0];
-            ks[1] = p[1];
+            const int64_t e = (((blk * hkv + h) * block_size) + tok % block_size) * kPD + kunit * 8;
+            if constexpr (FP8) {  // 16 fp8 -> 16 bf16 during staging: the LDS image and the math stay bf16
+                const uint4 v = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(kcv) + e);
+                ks[0] = __builtin_bit_cast(u16x8, fp8x8_to_bf16x8(v.x, v.y, k_scale));
+                ks[1] = __builtin_bit_cast(u16x8, fp8x8_to_bf16x8(v.z, v.w, k_scale));
+            } else {
+                const u16x8* p = reinterpret_cast<const u16x8*>(kc + e);
+                ks[0] = p[0];
+                ks[1] = p[1];
+            }
         } else {
             ks[0] = ks[1] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
         }
         const int vt = s * 32 + vhalf * 16;
         if (vt < kv_end) {
             const int64_t blk = bt[vt / block_size];
-            const u16x8* p = reinterpret_cast<const u16x8*>(vc + ((blk * hkv + h) * kPD + vrow) * (int64_t)block_size + vt % block_size);
-            vs[0] = p[0];
-            vs[1] = p[1];
+            const int64_t e = ((blk * hkv + h) * kPD + vrow) * (int64_t)block_size + vt % block_size;
+            if constexpr (FP8) {
+                const uint4 v = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(vcv) + e);
+                vs[0] = __builtin_bit_cast(u16x8, fp8x8_to_bf16x8(v.x, v.y, v_scale));
+                vs[1] = __builtin_bit_cast(u16x8, fp8x8_to_bf16x8(v.z, v.w, v_scale));
+            } else {
+                const u16x8* p = reinterpret_cast<const u16x8*>(vc + e);
+                vs[0] = p[0];
+                vs[1] = p[1];
+            }
         } else {
             vs[0] = vs[1] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
         }
@@ -204,18 +221,27 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(
     }
 }
 
-void launch_attn_prefill(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* block_table,
+void launch_attn_prefill(const uint16_t* q, const void* kc, const void* vc, const int32_t* block_table,
                          int bt_stride, const int32_t* q_start, const int32_t* ctx_len, const int32_t* tiles,
-                         int ntiles, uint16_t* out, int hq, int hkv, int block_size, float scale, hipStream_t st) {
+                         int ntiles, uint16_t* out, int hq, int hkv, int block_size, float scale, bool fp8,
+                         float k_scale, float v_scale, hipStream_t st) {
     if (ntiles == 0) return;
     static bool attr = [] {
-        return hipFuncSetAttribute((const void*)attn_prefill_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+        return hipFuncSetAttribute((const void*)attn_prefill_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   2 * kStage) == hipSuccess &&
+               hipFuncSetAttribute((const void*)attn_prefill_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                    2 * kStage) == hipSuccess;
     }();
     (void)attr;
-    hipLaunchKernelGGL(attn_prefill_kernel, dim3(ntiles, hkv), dim3(256), 2 * kStage, st, q, kc, vc, block_table,
-                       bt_stride, q_start, ctx_len, tiles, ntiles, out, hq, hkv, block_size,
-                       scale * 1.4426950408889634f);
+    const float sl = scale * 1.4426950408889634f;
+    if (fp8)
+        hipLaunchKernelGGL(attn_prefill_kernel<true>, dim3(ntiles, hkv), dim3(256), 2 * kStage, st, q, kc, vc,
+                           block_table, bt_stride, q_start, ctx_len, tiles, ntiles, out, hq, hkv, block_size, sl,
+                           k_scale, v_scale);
+    else
+        hipLaunchKernelGGL(attn_prefill_kernel<false>, dim3(ntiles, hkv), dim3(256), 2 * kStage, st, q, kc, vc,
+                           block_table, bt_stride, q_start, ctx_len, tiles, ntiles, out, hq, hkv, block_size, sl,
+                           1.f, 1.f);
 }
 
 }  // namespace chronos

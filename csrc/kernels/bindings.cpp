@@ -16,18 +16,19 @@ namespace chronos {
 void launch_embedding(const int32_t*, const uint16_t*, uint16_t*, int, int, int64_t, int64_t, hipStream_t);
 void launch_rmsnorm(const uint16_t*, uint16_t*, const uint16_t*, uint16_t*, int, int, float, hipStream_t);
 void launch_rope_kv_write(const uint16_t*, const int32_t*, const int32_t*, const int32_t*, int, const float*,
-                          uint16_t*, uint16_t*, uint16_t*, int, int, int, int, int, hipStream_t);
+                          uint16_t*, void*, void*, int, int, int, int, int, bool, float, float, hipStream_t);
 void launch_silu_mul(const uint16_t*, uint16_t*, int64_t, int, hipStream_t);
 size_t paged_attn_smem(int nqt);
-void launch_paged_attn(const uint16_t*, const uint16_t*, const uint16_t*, const int32_t*, int, const int32_t*,
+void launch_paged_attn(const uint16_t*, const void*, const void*, const int32_t*, int, const int32_t*,
                        const int32_t*, const int32_t*, int, int, int, uint16_t*, float*, float*, int, int, int, float,
-                       hipStream_t);
+                       bool, float, float, hipStream_t);
 void launch_constrained_sample(const void*, bool, int64_t, const int32_t*, int, int, const int16_t*, const int16_t*,
                                int, int32_t*, int32_t*, const float*, const int32_t*, int32_t*, int32_t*, int32_t*,
                                int32_t*, int32_t*, int, hipStream_t);
 void launch_gemv(const uint16_t*, int, int, const uint16_t*, int, uint16_t*, bool, hipStream_t);
-void launch_attn_prefill(const uint16_t*, const uint16_t*, const uint16_t*, const int32_t*, int, const int32_t*,
-                         const int32_t*, const int32_t*, int, uint16_t*, int, int, int, float, hipStream_t);
+void launch_attn_prefill(const uint16_t*, const void*, const void*, const int32_t*, int, const int32_t*,
+                         const int32_t*, const int32_t*, int, uint16_t*, int, int, int, float, bool, float, float,
+                         hipStream_t);
 }  // namespace chronos
 
 namespace {
@@ -52,6 +53,15 @@ inline void chk_bf16(const Tensor& t, const char* n) {
 inline void chk_i32(const Tensor& t, const char* n) {
     chk_gpu(t, n);
     CHK(t.scalar_type() == at::kInt, std::string(n) + " must be int32");
+}
+
+// KV caches are bf16 or fp8-e4m3 stored as uint8 (OCP e4m3fn bytes; dequantised with a per-layer scale)
+inline bool chk_kv(const Tensor& k, const Tensor& v) {
+    chk_gpu(k, "k_cache");
+    chk_gpu(v, "v_cache");
+    CHK(k.scalar_type() == v.scalar_type(), "k/v cache dtypes differ");
+    CHK(k.scalar_type() == at::kBFloat16 || k.scalar_type() == at::kByte, "kv cache must be bf16 or uint8 (fp8 e4m3)");
+    return k.scalar_type() == at::kByte;
 }
 
 Tensor embedding(const Tensor& ids, const Tensor& table, int64_t vstart) {
@@ -92,7 +102,7 @@ Tensor add_rmsnorm(const Tensor& x, const Tensor& resid, const Tensor& w, double
 
 void rope_kv_write(const Tensor& qkv, const Tensor& pos, const Tensor& tok_seq, const Tensor& block_table,
                    const Tensor& cos_sin, const Tensor& q_out, const Tensor& k_cache, const Tensor& v_cache, int64_t hq,
-                   int64_t hkv, bool write_q) {
+                   int64_t hkv, bool write_q, double k_scale, double v_scale) {
     chk_bf16(qkv, "qkv");
     chk_i32(pos, "pos");
     chk_i32(tok_seq, "tok_seq");
@@ -100,8 +110,7 @@ void rope_kv_write(const Tensor& qkv, const Tensor& pos, const Tensor& tok_seq, 
     chk_gpu(cos_sin, "cos_sin");
     CHK(cos_sin.scalar_type() == at::kFloat && cos_sin.dim() == 2 && cos_sin.size(1) == 128, "cos_sin [P,128] f32");
     chk_bf16(q_out, "q_out");
-    chk_bf16(k_cache, "k_cache");
-    chk_bf16(v_cache, "v_cache");
+    const bool fp8 = chk_kv(k_cache, v_cache);
     const int64_t t = qkv.size(0);
     CHK(qkv.dim() == 2 && qkv.size(1) == (hq + 2 * hkv) * 128, "qkv must be [T, (hq+2hkv)*128]");
     CHK(pos.numel() == t && tok_seq.numel() == t, "pos/tok_seq must have T entries");
@@ -112,8 +121,9 @@ void rope_kv_write(const Tensor& qkv, const Tensor& pos, const Tensor& tok_seq, 
     CHK(block_table.dim() == 2, "block_table [B, max_blocks]");
     c10::hip::HIPGuardMasqueradingAsCUDA g(qkv.device());
     chronos::launch_rope_kv_write(bf(qkv), i32(pos), i32(tok_seq), i32(block_table), (int)block_table.size(1),
-                                  cos_sin.data_ptr<float>(), bfm(q_out), bfm(k_cache), bfm(v_cache), (int)t, (int)hq,
-                                  (int)hkv, (int)k_cache.size(2), write_q ? 1 : 0, cur_stream());
+                                  cos_sin.data_ptr<float>(), bfm(q_out), k_cache.data_ptr(), v_cache.data_ptr(), (int)t,
+                                  (int)hq, (int)hkv, (int)k_cache.size(2), write_q ? 1 : 0, fp8, (float)k_scale,
+                                  (float)v_scale, cur_stream());
 }
 
 Tensor silu_mul(const Tensor& gu) {
@@ -130,10 +140,9 @@ Tensor silu_mul(const Tensor& gu) {
 
 Tensor paged_attention(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_table,
                        const Tensor& q_start, const Tensor& ctx_len, const c10::optional<Tensor>& tiles,
-                       int64_t ntiles, int64_t nqt, int64_t nsplit, double scale) {
+                       int64_t ntiles, int64_t nqt, int64_t nsplit, double scale, double k_scale, double v_scale) {
     chk_bf16(q, "q");
-    chk_bf16(k_cache, "k_cache");
-    chk_bf16(v_cache, "v_cache");
+    const bool fp8 = chk_kv(k_cache, v_cache);
     chk_i32(block_table, "block_table");
     chk_i32(q_start, "q_start");
     chk_i32(ctx_len, "ctx_len");
@@ -162,15 +171,17 @@ Tensor paged_attention(const Tensor& q, const Tensor& k_cache, const Tensor& v_c
     }
     if (nqt == 8) {  // flash prefill kernel: 128 query rows per workgroup, K/V tiles shared through LDS
         CHK(tp != nullptr, "nqt=8 (flash prefill) needs a tile list");
-        chronos::launch_attn_prefill(bf(q), bf(k_cache), bf(v_cache), i32(block_table), (int)block_table.size(1),
-                                     i32(q_start), i32(ctx_len), tp, (int)ntiles, bfm(out), (int)hq, (int)hkv,
-                                     (int)bs, (float)scale, cur_stream());
+        chronos::launch_attn_prefill(bf(q), k_cache.data_ptr(), v_cache.data_ptr(), i32(block_table),
+                                     (int)block_table.size(1), i32(q_start), i32(ctx_len), tp, (int)ntiles, bfm(out),
+                                     (int)hq, (int)hkv, (int)bs, (float)scale, fp8, (float)k_scale, (float)v_scale,
+                                     cur_stream());
         return out;
     }
-    chronos::launch_paged_attn(bf(q), bf(k_cache), bf(v_cache), i32(block_table), (int)block_table.size(1),
-                               i32(q_start), i32(ctx_len), tp, (int)ntiles, (int)nqt, (int)nsplit, bfm(out),
-                               nsplit > 1 ? po.data_ptr<float>() : nullptr, nsplit > 1 ? pl.data_ptr<float>() : nullptr,
-                               (int)hq, (int)hkv, (int)bs, (float)scale, cur_stream());
+    chronos::launch_paged_attn(bf(q), k_cache.data_ptr(), v_cache.data_ptr(), i32(block_table),
+                               (int)block_table.size(1), i32(q_start), i32(ctx_len), tp, (int)ntiles, (int)nqt,
+                               (int)nsplit, bfm(out), nsplit > 1 ? po.data_ptr<float>() : nullptr,
+                               nsplit > 1 ? pl.data_ptr<float>() : nullptr, (int)hq, (int)hkv, (int)bs, (float)scale,
+                               fp8, (float)k_scale, (float)v_scale, cur_stream());
     return out;
 }
 
@@ -240,11 +251,13 @@ TORCH_LIBRARY(chronos, m) {
     m.def("rmsnorm(Tensor x, Tensor w, float eps) -> Tensor");
     m.def("add_rmsnorm(Tensor x, Tensor(a!) resid, Tensor w, float eps) -> Tensor");
     m.def("rope_kv_write(Tensor qkv, Tensor pos, Tensor tok_seq, Tensor block_table, Tensor cos_sin, "
-          "Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, int hq, int hkv, bool write_q) -> ()");
+          "Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, int hq, int hkv, bool write_q, "
+          "float k_scale=1.0, float v_scale=1.0) -> ()");
     m.def("silu_mul(Tensor gate_up) -> Tensor");
     m.def("gemv(Tensor x, Tensor w, bool swiglu) -> Tensor");
     m.def("paged_attention(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_table, Tensor q_start, "
-          "Tensor ctx_len, Tensor? tiles, int ntiles, int nqt, int nsplit, float scale) -> Tensor");
+          "Tensor ctx_len, Tensor? tiles, int ntiles, int nqt, int nsplit, float scale, float k_scale=1.0, "
+          "float v_scale=1.0) -> Tensor");
     m.def("constrained_sample(Tensor logits, Tensor? row_of_slot, Tensor next, Tensor dist, int done_state, "
           "Tensor(a!) state, Tensor(b!) remaining, Tensor? temperature, Tensor? seed, Tensor(c!) ids, Tensor(d!) pos, "
           "Tensor(e!) ctx, Tensor(f!) nout, Tensor(g!) out_tokens) -> ()");

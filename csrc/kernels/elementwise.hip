@@ -82,7 +82,7 @@ __global__ void __launch_bounds__(256) rmsnorm_kernel(const uint16_t* __restrict
 }
 
 // ------------------------------------------------------------------------------------------------------------------
-// K4 RoPE + paged KV-cache write (+ K13 layout).  Input: the QKV GEMM output qkv[T, (Hq + 2*Hkv) * 128].
+// K4 RoPE + paged KV-cache write (+ K13: optional fp8-e4m3 cache with a per-layer scale).  Input: the QKV GEMM output qkv[T, (Hq + 2*Hkv) * 128].
 //   q  -> q_out[T, Hq, 128]                rotated (HF rotate-half convention)
 //   k  -> k_cache[blk, h, t % BS, :]        rotated       (row-major per token: B operand of S^T = K Q^T)
 //   v  -> v_cache[blk, h, :, t % BS]        transposed    (A operand of O^T = V^T P^T, see attention.hip)
@@ -90,11 +90,12 @@ __global__ void __launch_bounds__(256) rmsnorm_kernel(const uint16_t* __restrict
 // host-side slot mapping.  cos_sin[pos, 0:64] = cos, [64:128] = sin (f32, precomputed on the host incl. Llama-3.1
 // frequency scaling).  8 threads per head, each owning dims {8i..8i+7} and {64+8i..64+8i+7}.
 // ------------------------------------------------------------------------------------------------------------------
+template <bool FP8>
 __global__ void __launch_bounds__(256) rope_kv_write_kernel(
     const uint16_t* __restrict__ qkv, const int32_t* __restrict__ pos, const int32_t* __restrict__ tok_seq,
     const int32_t* __restrict__ block_table, int bt_stride, const float* __restrict__ cos_sin,
-    uint16_t* __restrict__ q_out, uint16_t* __restrict__ k_cache, uint16_t* __restrict__ v_cache, int hq, int hkv,
-    int block_size, int write_q) {
+    uint16_t* __restrict__ q_out, void* __restrict__ k_cache, void* __restrict__ v_cache, int hq, int hkv,
+    int block_size, int write_q, float k_inv_scale, float v_inv_scale) {
     constexpr int D = 128;
     const int t = blockIdx.x;
     const int unit = blockIdx.y * 32 + (threadIdx.x >> 3);  // head index over [q heads | k heads | v heads]
@@ -117,31 +118,61 @@ __global__ void __launch_bounds__(256) rope_kv_write_kernel(
         const float4 s1 = *reinterpret_cast<const float4*>(cs + 64 + 8 * i + 4);
         const float c[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
         const float s[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-        u16x8 ra, rb;
+        float fa[8], fb[8];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const float x1 = bf2f(a[j]), x2 = bf2f(b[j]);
-            ra[j] = f2bf(x1 * c[j] - x2 * s[j]);
-            rb[j] = f2bf(x2 * c[j] + x1 * s[j]);
+            fa[j] = x1 * c[j] - x2 * s[j];
+            fb[j] = x2 * c[j] + x1 * s[j];
         }
-        uint16_t* dst;
-        if (unit < hq) {
-            dst = q_out + ((int64_t)t * hq + unit) * D;
-        } else {
-            const int h = unit - hq;
-            dst = k_cache + (((blk * hkv + h) * block_size) + off) * D;
+        if (unit < hq || !FP8) {
+            u16x8 ra, rb;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                ra[j] = f2bf(fa[j]);
+                rb[j] = f2bf(fb[j]);
+            }
+            uint16_t* dst = unit < hq ? q_out + ((int64_t)t * hq + unit) * D
+                                      : reinterpret_cast<uint16_t*>(k_cache) +
+                                            (((blk * hkv + (unit - hq)) * block_size) + off) * D;
+            *reinterpret_cast<u16x8*>(dst + 8 * i) = ra;
+            *reinterpret_cast<u16x8*>(dst + 64 + 8 * i) = rb;
+        } else {  // fp8 K row: 128 bytes per token
+            uint8_t* dst = reinterpret_cast<uint8_t*>(k_cache) + (((blk * hkv + (unit - hq)) * block_size) + off) * D;
+            uint2 qa, qb;
+            qa.x = f32x4_to_fp8x4(fa[0] * k_inv_scale, fa[1] * k_inv_scale, fa[2] * k_inv_scale, fa[3] * k_inv_scale);
+            qa.y = f32x4_to_fp8x4(fa[4] * k_inv_scale, fa[5] * k_inv_scale, fa[6] * k_inv_scale, fa[7] * k_inv_scale);
+            qb.x = f32x4_to_fp8x4(fb[0] * k_inv_scale, fb[1] * k_inv_scale, fb[2] * k_inv_scale, fb[3] * k_inv_scale);
+            qb.y = f32x4_to_fp8x4(fb[4] * k_inv_scale, fb[5] * k_inv_scale, fb[6] * k_inv_scale, fb[7] * k_inv_scale);
+            *reinterpret_cast<uint2*>(dst + 8 * i) = qa;
+            *reinterpret_cast<uint2*>(dst + 64 + 8 * i) = qb;
         }
-        *reinterpret_cast<u16x8*>(dst + 8 * i) = ra;
-        *reinterpret_cast<u16x8*>(dst + 64 + 8 * i) = rb;
     } else {
         const int h = unit - hq - hkv;
         const u16x8 a = *reinterpret_cast<const u16x8*>(src + 16 * i);
         const u16x8 b = *reinterpret_cast<const u16x8*>(src + 16 * i + 8);
-        uint16_t* dst = v_cache + ((blk * hkv + h) * D) * (int64_t)block_size + off;
+        const int64_t base = ((blk * hkv + h) * D) * (int64_t)block_size + off;
+        if constexpr (FP8) {
+            uint8_t* dst = reinterpret_cast<uint8_t*>(v_cache) + base;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            dst[(int64_t)(16 * i + j) * block_size] = a[j];
-            dst[(int64_t)(16 * i + 8 + j) * block_size] = b[j];
+            for (int j = 0; j < 8; j += 4) {
+                const uint32_t qa = f32x4_to_fp8x4(bf2f(a[j]) * v_inv_scale, bf2f(a[j + 1]) * v_inv_scale,
+                                                   bf2f(a[j + 2]) * v_inv_scale, bf2f(a[j + 3]) * v_inv_scale);
+                const uint32_t qb = f32x4_to_fp8x4(bf2f(b[j]) * v_inv_scale, bf2f(b[j + 1]) * v_inv_scale,
+                                                   bf2f(b[j + 2]) * v_inv_scale, bf2f(b[j + 3]) * v_inv_scale);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    dst[(int64_t)(16 * i + j + e) * block_size] = (uint8_t)(qa >> (8 * e));
+                    dst[(int64_t)(16 * i + 8 + j + e) * block_size] = (uint8_t)(qb >> (8 * e));
+                }
+            }
+        } else {
+            uint16_t* dst = reinterpret_cast<uint16_t*>(v_cache) + base;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                dst[(int64_t)(16 * i + j) * block_size] = a[j];
+                dst[(int64_t)(16 * i + 8 + j) * block_size] = b[j];
+            }
         }
     }
 }
@@ -195,12 +226,18 @@ void launch_rmsnorm(const uint16_t* x, uint16_t* resid, const uint16_t* w, uint1
 }
 
 void launch_rope_kv_write(const uint16_t* qkv, const int32_t* pos, const int32_t* tok_seq, const int32_t* block_table,
-                          int bt_stride, const float* cos_sin, uint16_t* q_out, uint16_t* k_cache, uint16_t* v_cache,
-                          int t, int hq, int hkv, int block_size, int write_q, hipStream_t st) {
+                          int bt_stride, const float* cos_sin, uint16_t* q_out, void* k_cache, void* v_cache, int t,
+                          int hq, int hkv, int block_size, int write_q, bool fp8, float k_scale, float v_scale,
+                          hipStream_t st) {
     if (t == 0) return;
     const int nh = hq + 2 * hkv;
-    hipLaunchKernelGGL(rope_kv_write_kernel, dim3(t, (nh + 31) / 32), dim3(256), 0, st, qkv, pos, tok_seq,
-                       block_table, bt_stride, cos_sin, q_out, k_cache, v_cache, hq, hkv, block_size, write_q);
+    const dim3 g(t, (nh + 31) / 32), b(256);
+    if (fp8)
+        hipLaunchKernelGGL(rope_kv_write_kernel<true>, g, b, 0, st, qkv, pos, tok_seq, block_table, bt_stride, cos_sin,
+                           q_out, k_cache, v_cache, hq, hkv, block_size, write_q, 1.f / k_scale, 1.f / v_scale);
+    else
+        hipLaunchKernelGGL(rope_kv_write_kernel<false>, g, b, 0, st, qkv, pos, tok_seq, block_table, bt_stride,
+                           cos_sin, q_out, k_cache, v_cache, hq, hkv, block_size, write_q, 1.f, 1.f);
 }
 
 void launch_silu_mul(const uint16_t* gu, uint16_t* out, int64_t rows, int f, hipStream_t st) {

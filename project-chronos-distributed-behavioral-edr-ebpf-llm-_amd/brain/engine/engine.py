@@ -59,6 +59,8 @@ class EngineConfig:
     grammar_capacity: int = 2048
     max_string: int = 160          # default maxLength for schema strings without one (keeps verdicts short)
     prefix_cache: bool = True      # reuse KV blocks of identical prompt prefixes (the shared CHRONOS template head)
+    kv_dtype: str = "bf16"         # "bf16" or "fp8" (OCP e4m3fn, per-layer scale: half the KV bytes, 2x tokens/GPU)
+    kv_scale: float = 1.0          # fp8 KV scale (stored = value / scale)
     prefill_nqt: int = 8           # 8 = flash prefill kernel (128 query rows / workgroup); 1-2 = split-K kernel
 
 
@@ -123,7 +125,7 @@ class Engine:
             if self.device.type == "cuda":
                 free, _ = torch.cuda.mem_get_info(self.device)
                 budget = max(0.0, free * cfg.kv_fraction - cfg.reserve_gb * 2**30)
-                nb = int(budget // KVCache.bytes_per_block(mc, self.tp, bs))
+                nb = int(budget // KVCache.bytes_per_block(mc, self.tp, bs, cfg.kv_dtype))
                 nb = max(2, min(nb, need))
             else:
                 nb = need
@@ -133,7 +135,7 @@ class Engine:
             t = torch.tensor([nb], dtype=torch.int64, device=self.device)
             dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.tp.group)
             nb = int(t.item())
-        self.kv = KVCache(mc, self.tp, nb, bs, self.device)
+        self.kv = KVCache(mc, self.tp, nb, bs, self.device, cfg.kv_dtype, cfg.kv_scale, cfg.kv_scale)
         self.blocks = BlockManager(nb, bs, prefix_cache=cfg.prefix_cache)
         # ---- slot state (device) ----
         S, dev = cfg.max_slots, self.device

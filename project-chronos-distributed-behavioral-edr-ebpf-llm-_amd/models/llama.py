@@ -363,18 +363,22 @@ class KVCache:
     """
 
     def __init__(self, cfg: LlamaConfig, tp: TPContext, num_blocks: int, block_size: int = 16, device="cpu",
-                 dtype=torch.bfloat16):
+                 dtype: str = "bf16", k_scale: float = 1.0, v_scale: float = 1.0):
         _, hkv = _local_heads(cfg, tp)
         self.num_blocks, self.block_size, self.hkv = num_blocks, block_size, hkv
+        self.dtype = dtype
         per = hkv * block_size * cfg.head_dim
-        self.buf = torch.zeros(cfg.num_layers, 2, num_blocks, per, device=device, dtype=dtype)
+        tdt = torch.uint8 if dtype == "fp8" else torch.bfloat16  # fp8 = OCP e4m3fn bytes + per-layer scale
+        self.buf = torch.zeros(cfg.num_layers, 2, num_blocks, per, device=device, dtype=tdt)
+        self.k_scale = [float(k_scale)] * cfg.num_layers
+        self.v_scale = [float(v_scale)] * cfg.num_layers
         self.k = [self.buf[l, 0].view(num_blocks, hkv, block_size, cfg.head_dim) for l in range(cfg.num_layers)]
         self.v = [self.buf[l, 1].view(num_blocks, hkv, cfg.head_dim, block_size) for l in range(cfg.num_layers)]
 
     @staticmethod
-    def bytes_per_block(cfg: LlamaConfig, tp: TPContext, block_size: int = 16) -> int:
+    def bytes_per_block(cfg: LlamaConfig, tp: TPContext, block_size: int = 16, dtype: str = "bf16") -> int:
         _, hkv = _local_heads(cfg, tp)
-        return cfg.num_layers * 2 * hkv * block_size * cfg.head_dim * 2
+        return cfg.num_layers * 2 * hkv * block_size * cfg.head_dim * (1 if dtype == "fp8" else 2)
 
 
 @dataclass
@@ -453,9 +457,9 @@ class LlamaModel:
         for li, lw in enumerate(w.layers):
             qkv = ops.linear(x, lw.wqkv)
             ops.rope_kv_write(qkv, sb.pos, sb.tok_seq, sb.block_table, self.cos_sin, q_buf, kv.k[li], kv.v[li],
-                              self.hq, self.hkv, True)
+                              self.hq, self.hkv, True, kv.k_scale[li], kv.v_scale[li])
             attn = ops.paged_attention(q_buf, kv.k[li], kv.v[li], sb.block_table, sb.q_start, sb.ctx_len, sb.tiles,
-                                       sb.ntiles, sb.nqt, sb.nsplit, self.scale)
+                                       sb.ntiles, sb.nqt, sb.nsplit, self.scale, kv.k_scale[li], kv.v_scale[li])
             o = tp.all_reduce(ops.linear(attn.view(T, -1), lw.wo))
             x = ops.add_rmsnorm(o, resid, lw.mlp_norm, eps)
             a = ops.gate_up_silu(x, lw.w_gu)

@@ -59,20 +59,25 @@ def silu_mul(gu: torch.Tensor) -> torch.Tensor:
 
 
 def rope_kv_write(qkv, pos, tok_seq, block_table, cos_sin, q_out, k_cache, v_cache, hq: int, hkv: int,
-                  write_q: bool = True) -> None:
+                  write_q: bool = True, k_scale: float = 1.0, v_scale: float = 1.0) -> None:
+    """RoPE q/k + write k/v into the paged cache (bf16, or fp8-e4m3 bytes when the cache is uint8)."""
     if qkv.is_cuda:
-        _k().rope_kv_write(qkv, pos, tok_seq, block_table, cos_sin, q_out, k_cache, v_cache, hq, hkv, write_q)
+        _k().rope_kv_write(qkv, pos, tok_seq, block_table, cos_sin, q_out, k_cache, v_cache, hq, hkv, write_q,
+                           k_scale, v_scale)
     else:
-        ref.rope_kv_write(qkv, pos, tok_seq, block_table, cos_sin, q_out, k_cache, v_cache, hq, hkv, write_q)
+        ref.rope_kv_write(qkv, pos, tok_seq, block_table, cos_sin, q_out, k_cache, v_cache, hq, hkv, write_q,
+                          k_scale, v_scale)
 
 
 def paged_attention(q, k_cache, v_cache, block_table, q_start, ctx_len, tiles=None, ntiles: int = 0, nqt: int = 1,
-                    nsplit: int = 1, scale: float | None = None) -> torch.Tensor:
+                    nsplit: int = 1, scale: float | None = None, k_scale: float = 1.0,
+                    v_scale: float = 1.0) -> torch.Tensor:
     scale = scale if scale is not None else 1.0 / math.sqrt(q.shape[-1])
     if q.is_cuda:
         return _k().paged_attention(q, k_cache, v_cache, block_table, q_start, ctx_len, tiles, ntiles, nqt, nsplit,
-                                    scale)
-    return ref.paged_attention(q, k_cache, v_cache, block_table, q_start, ctx_len, tiles, ntiles, nqt, nsplit, scale)
+                                    scale, k_scale, v_scale)
+    return ref.paged_attention(q, k_cache, v_cache, block_table, q_start, ctx_len, tiles, ntiles, nqt, nsplit, scale,
+                               k_scale, v_scale)
 
 
 def constrained_sample(logits, row_of_slot, next_tab, dist, done_state: int, state, remaining, temperature, seed,

@@ -34,8 +34,20 @@ def silu_mul(gu: torch.Tensor) -> torch.Tensor:
     return (torch.nn.functional.silu(g).to(torch.bfloat16).float() * u).to(gu.dtype)
 
 
+FP8_MAX = 448.0
+
+
+def to_fp8_bytes(x: torch.Tensor, inv_scale: float) -> torch.Tensor:
+    """f32 -> OCP e4m3fn bytes with saturation (what the HIP kernels store)."""
+    return (x.float() * inv_scale).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn).view(torch.uint8)
+
+
+def from_fp8_bytes(b: torch.Tensor, scale: float) -> torch.Tensor:
+    return b.view(torch.float8_e4m3fn).float() * scale
+
+
 def rope_kv_write(qkv, pos, tok_seq, block_table, cos_sin, q_out, k_cache, v_cache, hq: int, hkv: int,
-                  write_q: bool = True) -> None:
+                  write_q: bool = True, k_scale: float = 1.0, v_scale: float = 1.0) -> None:
     T = qkv.shape[0]
     D = 128
     x = qkv.view(T, hq + 2 * hkv, D).float()
@@ -50,13 +62,18 @@ def rope_kv_write(qkv, pos, tok_seq, block_table, cos_sin, q_out, k_cache, v_cac
     bs = k_cache.shape[2]
     blk = block_table[tok_seq.long(), p // bs].long()
     off = p % bs
-    k_cache[blk, :, off, :] = rot[:, hq:]
     v = x[:, hq + hkv:].to(torch.bfloat16)  # [T, hkv, D]
-    v_cache[blk, :, :, off] = v
+    if k_cache.dtype == torch.uint8:
+        rotf = torch.cat([x1 * cos - x2 * sin, x2 * cos + x1 * sin], dim=-1)
+        k_cache[blk, :, off, :] = to_fp8_bytes(rotf[:, hq:], 1.0 / k_scale)
+        v_cache[blk, :, :, off] = to_fp8_bytes(v, 1.0 / v_scale)
+    else:
+        k_cache[blk, :, off, :] = rot[:, hq:]
+        v_cache[blk, :, :, off] = v
 
 
 def paged_attention(q, k_cache, v_cache, block_table, q_start, ctx_len, tiles=None, ntiles=0, nqt=1, nsplit=1,
-                    scale: float | None = None) -> torch.Tensor:
+                    scale: float | None = None, k_scale: float = 1.0, v_scale: float = 1.0) -> torch.Tensor:
     """Causal varlen attention over the paged cache.  q [T, Hq, 128]; seqs given by q_start/ctx_len."""
     T, hq, D = q.shape
     hkv, bs = k_cache.shape[1], k_cache.shape[2]
@@ -77,8 +94,12 @@ def paged_attention(q, k_cache, v_cache, block_table, q_start, ctx_len, tiles=No
         ctx = int(ctx_len[b])
         nblk = (ctx + bs - 1) // bs
         blks = bt[b, :nblk]
-        K = k_cache[blks].permute(1, 0, 2, 3).reshape(hkv, nblk * bs, D)[:, :ctx].float()
-        V = v_cache[blks].permute(1, 0, 3, 2).reshape(hkv, nblk * bs, D)[:, :ctx].float()
+        kb, vb = k_cache[blks], v_cache[blks]
+        if k_cache.dtype == torch.uint8:  # fp8 cache: dequantise like the kernel (value * scale, then bf16)
+            kb = from_fp8_bytes(kb, k_scale).to(torch.bfloat16)
+            vb = from_fp8_bytes(vb, v_scale).to(torch.bfloat16)
+        K = kb.permute(1, 0, 2, 3).reshape(hkv, nblk * bs, D)[:, :ctx].float()
+        V = vb.permute(1, 0, 3, 2).reshape(hkv, nblk * bs, D)[:, :ctx].float()
         qq = q[q0:q1].float().view(ql, hkv, G, D)
         s = torch.einsum("qhgd,hkd->hgqk", qq, K) * scale
         qpos = torch.arange(ctx - ql, ctx, device=q.device)

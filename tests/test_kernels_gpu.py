@@ -291,3 +291,67 @@ def test_gemv_fused_swiglu(m):
     exp = ref.silu_mul((x.float() @ w.float().t()).to(torch.bfloat16))
     _close(y, exp, 2e-2, 3e-2)
     assert ops.gate_up_silu(x, w).shape == (m, 1792)
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# fp8-e4m3 (OCP) KV cache
+# ---------------------------------------------------------------------------------------------------------------
+
+def test_fp8_conversion_is_ocp_e4m3fn():
+    """The cache bytes written by the kernel must decode with torch.float8_e4m3fn (OCP), not the MI300 fnuz format."""
+    from chronos import ops
+    from chronos.models.llama import get_config, rope_table
+    from chronos.ops import reference as ref
+
+    g = torch.Generator(device=DEV).manual_seed(5)
+    hq, hkv, bs, T = 32, 8, 16, 20
+    cs = rope_table(get_config("llama3-8b"), 512, DEV)
+    qkv = (torch.randn(T, (hq + 2 * hkv) * 128, device=DEV, generator=g) * 3).to(torch.bfloat16)
+    pos = torch.arange(T, device=DEV, dtype=torch.int32)
+    bt = torch.arange(4, device=DEV, dtype=torch.int32).view(1, 4)
+    ts = torch.zeros(T, dtype=torch.int32, device=DEV)
+    k1 = torch.zeros(4, hkv, bs, 128, dtype=torch.uint8, device=DEV)
+    v1 = torch.zeros(4, hkv, 128, bs, dtype=torch.uint8, device=DEV)
+    k2, v2 = k1.clone(), v1.clone()
+    q1 = torch.empty(T, hq, 128, device=DEV, dtype=torch.bfloat16)
+    q2 = torch.empty_like(q1)
+    ops.rope_kv_write(qkv, pos, ts, bt, cs, q1, k1, v1, hq, hkv, True, 0.5, 2.0)
+    ref.rope_kv_write(qkv, pos, ts, bt, cs, q2, k2, v2, hq, hkv, True, 0.5, 2.0)
+    assert torch.equal(v1, v2)
+    kd1, kd2 = ref.from_fp8_bytes(k1, 0.5), ref.from_fp8_bytes(k2, 0.5)
+    # rounding of the rotated value may differ in the last fp8 ulp (f32 vs reference op order)
+    assert (kd1 - kd2).abs().max() <= 0.0625 * kd2.abs().max()
+    assert (k1 != k2).float().mean() < 0.01
+
+
+@pytest.mark.parametrize("nqt", [1, 8])
+def test_fp8_paged_attention(nqt):
+    from chronos import ops
+    from chronos.ops import reference as ref
+
+    q_lens, ctx_lens = ([1] * 5, [1, 17, 200, 513, 1000]) if nqt == 1 else ([33, 100], [90, 300])
+    q, k, v, bt, qs, ctx = _attn_case(q_lens, ctx_lens, 32, 8, 16, seed=13)
+    k8 = ref.to_fp8_bytes(k, 1 / 0.25)
+    v8 = ref.to_fp8_bytes(v, 1 / 0.5)
+    if nqt == 1:
+        tt, nt = None, len(q_lens)
+    else:
+        tiles = ops.attention_tiles(q_lens, 32, 8, nqt)
+        tt, nt = torch.tensor(tiles, dtype=torch.int32, device=DEV).view(-1, 2), len(tiles)
+    out = ops.paged_attention(q, k8, v8, bt, qs, ctx, tt, nt, nqt, 2 if nqt == 1 else 1, None, 0.25, 0.5)
+    exp = ref.paged_attention(q, k8, v8, bt, qs, ctx, tt, nt, nqt, 1, None, 0.25, 0.5)
+    _close(out, exp, 2e-2, 2e-2)
+
+
+def test_engine_fp8_kv_end_to_end():
+    import json
+
+    from chronos.brain.engine.engine import Engine, EngineConfig
+    from chronos.sensor.prompt import VERDICT_SCHEMA, build_prompt
+
+    eng = Engine(EngineConfig(model="small", device=DEV, max_slots=4, max_model_len=256, kv_dtype="fp8",
+                              decode_burst=4))
+    assert eng.kv.buf.dtype == torch.uint8
+    r = eng.submit(build_prompt(["[EXEC] bash -> curl", "[OPEN] curl -> /tmp/x"]), fmt=VERDICT_SCHEMA, num_predict=40)
+    eng.run_until_idle()
+    assert {"risk_score", "verdict", "reason"} <= set(json.loads(r.text))
