@@ -23,8 +23,8 @@ void launch_paged_attn(const uint16_t*, const void*, const void*, const int32_t*
                        const int32_t*, const int32_t*, int, int, int, uint16_t*, float*, float*, int, int, int, float,
                        bool, float, float, hipStream_t);
 void launch_constrained_sample(const void*, bool, int64_t, const int32_t*, int, int, const int16_t*, const int16_t*,
-                               int, int32_t*, int32_t*, const float*, const int32_t*, int32_t*, int32_t*, int32_t*,
-                               int32_t*, int32_t*, int, hipStream_t);
+                               int, int32_t*, int32_t*, const float*, const int32_t*, const int32_t*, const float*,
+                               int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, int, hipStream_t);
 void launch_gemv(const uint16_t*, int, int, const uint16_t*, int, uint16_t*, bool, hipStream_t);
 void launch_attn_prefill(const uint16_t*, const void*, const void*, const int32_t*, int, const int32_t*,
                          const int32_t*, const int32_t*, int, uint16_t*, int, int, int, float, bool, float, float,
@@ -188,7 +188,8 @@ Tensor paged_attention(const Tensor& q, const Tensor& k_cache, const Tensor& v_c
 void constrained_sample(const Tensor& logits, const c10::optional<Tensor>& row_of_slot, const Tensor& next,
                         const Tensor& dist, int64_t done_state, const Tensor& state, const Tensor& remaining,
                         const c10::optional<Tensor>& temperature, const c10::optional<Tensor>& seed, const Tensor& ids,
-                        const Tensor& pos, const Tensor& ctx, const Tensor& nout, const Tensor& out_tokens) {
+                        const Tensor& pos, const Tensor& ctx, const Tensor& nout, const Tensor& out_tokens,
+                        const c10::optional<Tensor>& topk, const c10::optional<Tensor>& topp) {
     CHK(logits.is_cuda() && logits.dim() == 2 && logits.stride(1) == 1, "logits [rows, V] row-contiguous");
     CHK(logits.scalar_type() == at::kBFloat16 || logits.scalar_type() == at::kFloat, "logits bf16 or f32");
     chk_gpu(next, "next");
@@ -222,11 +223,24 @@ void constrained_sample(const Tensor& logits, const c10::optional<Tensor>& row_o
         chk_i32(*seed, "seed");
         sp = i32(*seed);
     }
+    const int32_t* kp = nullptr;
+    if (topk.has_value()) {
+        chk_i32(*topk, "topk");
+        CHK(topk->numel() >= n, "topk: one entry per slot");
+        kp = i32(*topk);
+    }
+    const float* pp = nullptr;
+    if (topp.has_value()) {
+        chk_gpu(*topp, "topp");
+        CHK(topp->scalar_type() == at::kFloat && topp->numel() >= n, "topp: f32, one entry per slot");
+        pp = topp->data_ptr<float>();
+    }
     c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
     chronos::launch_constrained_sample(logits.data_ptr(), logits.scalar_type() == at::kFloat, logits.stride(0), rp,
                                        (int)n, (int)vocab, next.data_ptr<int16_t>(), dist.data_ptr<int16_t>(),
-                                       (int)done_state, i32m(state), i32m(remaining), tp, sp, i32m(ids), i32m(pos),
-                                       i32m(ctx), i32m(nout), i32m(out_tokens), (int)out_tokens.size(1), cur_stream());
+                                       (int)done_state, i32m(state), i32m(remaining), tp, sp, kp, pp, i32m(ids),
+                                       i32m(pos), i32m(ctx), i32m(nout), i32m(out_tokens), (int)out_tokens.size(1),
+                                       cur_stream());
 }
 
 // y = x @ w.T for M <= 8 rows (decode); swiglu: w = [gate; up] -> y = silu(x@gate.T) * (x@up.T)
@@ -260,7 +274,7 @@ TORCH_LIBRARY(chronos, m) {
           "float v_scale=1.0) -> Tensor");
     m.def("constrained_sample(Tensor logits, Tensor? row_of_slot, Tensor next, Tensor dist, int done_state, "
           "Tensor(a!) state, Tensor(b!) remaining, Tensor? temperature, Tensor? seed, Tensor(c!) ids, Tensor(d!) pos, "
-          "Tensor(e!) ctx, Tensor(f!) nout, Tensor(g!) out_tokens) -> ()");
+          "Tensor(e!) ctx, Tensor(f!) nout, Tensor(g!) out_tokens, Tensor? topk=None, Tensor? topp=None) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(chronos, CUDA, m) {

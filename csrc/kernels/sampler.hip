@@ -6,7 +6,8 @@
 //   dist[S]    int16   fewest tokens that lead from s to DONE (EOS included); DONE has dist 0
 // Per row b the kernel picks argmax_v score(v) over legal v with dist[next[s][v]] <= remaining[b] - 1 ("budget
 // forcing": the verdict always closes within max_tokens), where score = logit (greedy) or logit / T + Gumbel noise
-// (exact sampling from softmax(logit / T) via the Gumbel-max trick, counter-based RNG, so replays are reproducible).
+// (exact sampling from softmax(logit / T) via the Gumbel-max trick, counter-based RNG, so replays are reproducible),
+// optionally restricted to the top-k / top-p nucleus (Ollama options) by an exact radix select on the logit keys.
 //
 // It then advances the per-slot decode state in place — ids, positions, context length, DFA state, budget, output
 // ring — so a captured decode graph can be replayed for many steps with no host round trip.  Rows whose state is
@@ -31,15 +32,27 @@ __device__ __forceinline__ float logit_at<uint16_t>(const uint16_t* p, int64_t i
 template <>
 __device__ __forceinline__ float logit_at<float>(const float* p, int64_t i) { return p[i]; }
 
+// Monotone 16-bit key of a logit (its bf16 rounding): larger key <=> larger value.  Ranks for top-k / top-p.
+__device__ __forceinline__ uint32_t ord_key(float x) {
+    const uint32_t b = f2bf(x);
+    return (b & 0x8000u) ? (~b & 0xFFFFu) : (b | 0x8000u);
+}
+
 template <typename LT>
 __global__ void __launch_bounds__(1024) constrained_sample_kernel(
     const LT* __restrict__ logits, int64_t lstride, const int32_t* __restrict__ row_of_slot, int vocab,
     const int16_t* __restrict__ next, const int16_t* __restrict__ dist, int done_state, int32_t* __restrict__ state,
     int32_t* __restrict__ remaining, const float* __restrict__ temperature, const int32_t* __restrict__ seed,
+    const int32_t* __restrict__ topk, const float* __restrict__ topp,
     int32_t* __restrict__ ids, int32_t* __restrict__ pos, int32_t* __restrict__ ctx, int32_t* __restrict__ nout,
     int32_t* __restrict__ out_tokens, int max_out) {
     __shared__ float bv[16];
     __shared__ int bi[16];
+    __shared__ int hc[256];
+    __shared__ float hm[256];
+    __shared__ uint32_t sh_thr, sh_bk, sh_bp;
+    __shared__ int sh_above_k;
+    __shared__ float sh_above_p, sh_target_p;
     const int slot = blockIdx.x;
     const int s = state[slot];
     if (s < 0 || s == done_state) return;
@@ -52,13 +65,114 @@ __global__ void __launch_bounds__(1024) constrained_sample_kernel(
     const float invt = temp > 0.f ? 1.f / temp : 0.f;
     const uint32_t key = mix32((uint32_t)(seed ? seed[slot] : 0) * 0x9E3779B9U ^ (uint32_t)nout[slot] * 0x85EBCA6BU ^
                                (uint32_t)slot);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    auto legal = [&](int v) {
+        const int ns = nx[v];
+        return ns >= 0 && dist[ns] <= budget;
+    };
 
+    // ---- optional top-k / top-p (llama.cpp order: on the raw logits, before temperature) -------------------------
+    // Exact two-level radix select on the 16-bit keys: a 256-bin histogram of the high byte (counts and softmax mass),
+    // then one of the low byte inside the bin that crosses k (resp. p * Z).  Tokens with key >= threshold survive.
+    const int tk = topk ? topk[slot] : 0;
+    const float tp = topp ? topp[slot] : 1.f;
+    uint32_t thr = 0;
+    if (temp > 0.f && (tk > 0 || tp < 1.f)) {
+        float mx = -INFINITY;
+        for (int v = threadIdx.x; v < vocab; v += blockDim.x)
+            if (legal(v)) mx = fmaxf(mx, logit_at<LT>(lg, v));
+        mx = wave_max(mx);
+        if (lane == 0) bv[w] = mx;
+        for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+            hc[i] = 0;
+            hm[i] = 0.f;
+        }
+        __syncthreads();
+        mx = bv[0];
+        for (int k = 1; k < nw; ++k) mx = fmaxf(mx, bv[k]);
+        for (int v = threadIdx.x; v < vocab; v += blockDim.x)
+            if (legal(v)) {
+                const float x = logit_at<LT>(lg, v);
+                const uint32_t kk = ord_key(x) >> 8;
+                atomicAdd(&hc[kk], 1);
+                atomicAdd(&hm[kk], __expf(x - mx));
+            }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            float z = 0.f;
+            for (int i = 0; i < 256; ++i) z += hm[i];
+            int cnt = 0;
+            float mass = 0.f;
+            uint32_t bk = 0xFFFFFFFFu, bp = 0xFFFFFFFFu;
+            for (int i = 255; i >= 0; --i) {
+                if (tk > 0 && bk == 0xFFFFFFFFu && cnt + hc[i] >= tk) {
+                    bk = i;
+                    sh_above_k = cnt;
+                }
+                if (tp < 1.f && bp == 0xFFFFFFFFu && mass + hm[i] >= tp * z) {
+                    bp = i;
+                    sh_above_p = mass;
+                }
+                cnt += hc[i];
+                mass += hm[i];
+            }
+            sh_bk = bk;
+            sh_bp = bp;
+            sh_target_p = tp * z;
+        }
+        __syncthreads();
+        const uint32_t bk = sh_bk, bp = sh_bp;
+        for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+            hc[i] = 0;
+            hm[i] = 0.f;
+        }
+        __syncthreads();
+        if (bk != 0xFFFFFFFFu || bp != 0xFFFFFFFFu) {
+            for (int v = threadIdx.x; v < vocab; v += blockDim.x)
+                if (legal(v)) {
+                    const float x = logit_at<LT>(lg, v);
+                    const uint32_t kk = ord_key(x);
+                    if ((kk >> 8) == bk) atomicAdd(&hc[kk & 255], 1);
+                    if ((kk >> 8) == bp) atomicAdd(&hm[kk & 255], __expf(x - mx));
+                }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t t = 0;
+            if (bk != 0xFFFFFFFFu) {
+                int cnt = sh_above_k;
+                for (int i = 255; i >= 0; --i) {
+                    cnt += hc[i];
+                    if (cnt >= tk) {
+                        t = (bk << 8) | (uint32_t)i;
+                        break;
+                    }
+                }
+            }
+            if (bp != 0xFFFFFFFFu) {
+                float mass = sh_above_p;
+                for (int i = 255; i >= 0; --i) {
+                    mass += hm[i];
+                    if (mass >= sh_target_p) {
+                        const uint32_t tpk = (bp << 8) | (uint32_t)i;
+                        t = t > tpk ? t : tpk;
+                        break;
+                    }
+                }
+            }
+            sh_thr = t;
+        }
+        __syncthreads();
+        thr = sh_thr;
+    }
+
+    // ---- greedy / Gumbel-max over the legal (and, if filtered, surviving) tokens ---------------------------------
     float best = -INFINITY;
     int besti = 0x7fffffff;
     for (int v = threadIdx.x; v < vocab; v += blockDim.x) {
-        const int ns = nx[v];
-        if (ns < 0 || dist[ns] > budget) continue;
+        if (!legal(v)) continue;
         float sc = logit_at<LT>(lg, v);
+        if (thr && ord_key(sc) < thr) continue;
         if (temp > 0.f) {
             const uint32_t hsh = mix32(key ^ (uint32_t)v * 0xC2B2AE35U);
             const float u = ((hsh >> 8) + 0.5f) * (1.f / 16777216.f);
@@ -78,14 +192,13 @@ __global__ void __launch_bounds__(1024) constrained_sample_kernel(
             besti = oi;
         }
     }
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    __syncthreads();  // bv/bi may still be read by the top-k pass above
     if (lane == 0) {
         bv[w] = best;
         bi[w] = besti;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        const int nw = blockDim.x >> 6;
         for (int k = 1; k < nw; ++k)
             if (bv[k] > best || (bv[k] == best && bi[k] < besti)) {
                 best = bv[k];
@@ -112,17 +225,17 @@ __global__ void __launch_bounds__(1024) constrained_sample_kernel(
 void launch_constrained_sample(const void* logits, bool logits_f32, int64_t lstride, const int32_t* row_of_slot,
                                int nslots, int vocab, const int16_t* next, const int16_t* dist, int done_state,
                                int32_t* state, int32_t* remaining, const float* temperature, const int32_t* seed,
-                               int32_t* ids, int32_t* pos, int32_t* ctx, int32_t* nout, int32_t* out_tokens,
-                               int max_out, hipStream_t st) {
+                               const int32_t* topk, const float* topp, int32_t* ids, int32_t* pos, int32_t* ctx,
+                               int32_t* nout, int32_t* out_tokens, int max_out, hipStream_t st) {
     if (nslots == 0) return;
     if (logits_f32)
         hipLaunchKernelGGL(constrained_sample_kernel<float>, dim3(nslots), dim3(1024), 0, st,
                            (const float*)logits, lstride, row_of_slot, vocab, next, dist, done_state, state, remaining,
-                           temperature, seed, ids, pos, ctx, nout, out_tokens, max_out);
+                           temperature, seed, topk, topp, ids, pos, ctx, nout, out_tokens, max_out);
     else
         hipLaunchKernelGGL(constrained_sample_kernel<uint16_t>, dim3(nslots), dim3(1024), 0, st,
                            (const uint16_t*)logits, lstride, row_of_slot, vocab, next, dist, done_state, state,
-                           remaining, temperature, seed, ids, pos, ctx, nout, out_tokens, max_out);
+                           remaining, temperature, seed, topk, topp, ids, pos, ctx, nout, out_tokens, max_out);
 }
 
 }  // namespace chronos

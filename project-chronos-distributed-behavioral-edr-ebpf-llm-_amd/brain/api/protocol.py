@@ -30,6 +30,8 @@ class GenerateParams:
     num_predict: int = 0
     temperature: float = 0.0
     seed: int = 0
+    top_k: int = 0
+    top_p: float = 1.0
 
     @classmethod
     def parse(cls, body: dict, chat: bool = False, default_temperature: float = 0.0) -> "GenerateParams":
@@ -52,6 +54,9 @@ class GenerateParams:
             temperature=float(opts.get("temperature", default_temperature)),
             seed=int(opts.get("seed", 0) or 0),
         )
+        if p.temperature > 0:  # Ollama's sampler defaults apply whenever it samples (top_k 40, top_p 0.9)
+            p.top_k = int(opts.get("top_k", 40) or 0)
+            p.top_p = float(opts.get("top_p", 0.9))
         if chat:
             msgs = body.get("messages")
             if not isinstance(msgs, list) or not msgs:

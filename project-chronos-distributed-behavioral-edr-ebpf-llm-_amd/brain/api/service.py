@@ -55,7 +55,7 @@ class EngineService:
     def _admit(self, item) -> None:
         params, ids, on_done, on_tokens = item
         self.engine.submit(ids, fmt=params.format, num_predict=params.num_predict, temperature=params.temperature,
-                           seed=params.seed, callback=on_done, meta={"on_tokens": on_tokens} if on_tokens else None)
+                           seed=params.seed, top_k=params.top_k, top_p=params.top_p, callback=on_done, meta={"on_tokens": on_tokens} if on_tokens else None)
 
     def close(self) -> None:
         self._stop.set()

@@ -74,6 +74,8 @@ class Request:
     seed: int = 0
     callback: Optional[Callable[["Request"], None]] = None
     meta: dict = field(default_factory=dict)
+    top_k: int = 0                 # 0 = off
+    top_p: float = 1.0             # 1.0 = off
     # runtime
     slot: int = -1
     blocks: list = field(default_factory=list)
@@ -148,6 +150,8 @@ class Engine:
         self.s_nout = torch.zeros(S, **i32)
         self.s_seed = torch.zeros(S, **i32)
         self.s_temp = torch.zeros(S, dtype=torch.float32, device=dev)
+        self.s_topk = torch.zeros(S, **i32)
+        self.s_topp = torch.ones(S, dtype=torch.float32, device=dev)
         self.s_out = torch.zeros(S, cfg.max_out, **i32)
         self.s_bt = torch.zeros(S, self.max_blocks_per_seq, **i32)
         self.s_row = torch.full((S,), -1, **i32)
@@ -171,11 +175,13 @@ class Engine:
     # ------------------------------------------------------------------------------------------------------------
     def submit(self, prompt: str | list, fmt=None, num_predict: int | None = None, temperature: float = 0.0,
                seed: int = 0, raw: bool = False, system: str | None = None,
-               callback: Callable[[Request], None] | None = None, meta: dict | None = None) -> Request:
+               callback: Callable[[Request], None] | None = None, meta: dict | None = None, top_k: int = 0,
+               top_p: float = 1.0) -> Request:
         ids = prompt if isinstance(prompt, list) else self.tok.chat_ids(prompt, system=system, raw=raw)
         n = num_predict if num_predict and num_predict > 0 else self.cfg.default_num_predict
         n = min(n, self.cfg.max_out, self.cfg.max_model_len - len(ids))
         req = Request(next(self._rid), ids, fmt, n, float(temperature or 0.0), int(seed or 0), callback, meta or {})
+        req.top_k, req.top_p = int(top_k or 0), float(top_p if top_p is not None else 1.0)
         req.t_submit = time.perf_counter()
         if n <= 0:
             req.error = f"prompt of {len(ids)} tokens exceeds max_model_len {self.cfg.max_model_len}"
@@ -286,10 +292,13 @@ class Engine:
         self.s_nout[sl] = 0
         self.s_temp[sl] = dv(torch.tensor([r.temperature for r in done_reqs], dtype=torch.float32))
         self.s_seed[sl] = dv(torch.tensor([r.seed for r in done_reqs], dtype=torch.int32))
+        self.s_topk[sl] = dv(torch.tensor([r.top_k for r in done_reqs], dtype=torch.int32))
+        self.s_topp[sl] = dv(torch.tensor([r.top_p for r in done_reqs], dtype=torch.float32))
         self.s_row.fill_(-1)
         self.s_row[sl] = dv(torch.tensor(done_rows, dtype=torch.int32))
         ops.constrained_sample(logits, self.s_row, self.bank.next, self.bank.dist, DONE, self.s_state, self.s_rem,
-                               self.s_temp, self.s_seed, self.s_ids, self.s_pos, self.s_ctx, self.s_nout, self.s_out)
+                               self.s_temp, self.s_seed, self.s_ids, self.s_pos, self.s_ctx, self.s_nout, self.s_out,
+                               self.s_topk, self.s_topp)
         now = time.perf_counter()
         for r in done_reqs:
             r.t_first = now
@@ -305,7 +314,7 @@ class Engine:
         logits = self.model.forward(sb, self.kv)
         ops.constrained_sample(logits, None, self.bank.next, self.bank.dist, DONE, self.s_state[:n], self.s_rem[:n],
                                self.s_temp[:n], self.s_seed[:n], self.s_ids[:n], self.s_pos[:n], self.s_ctx[:n],
-                               self.s_nout[:n], self.s_out[:n])
+                               self.s_nout[:n], self.s_out[:n], self.s_topk[:n], self.s_topp[:n])
 
     def _nsplit(self, n: int) -> int:
         return ops.pick_nsplit(n * self.model.hkv, self.cfg.max_model_len)
@@ -408,7 +417,7 @@ class Engine:
         si = torch.tensor(movers, dtype=torch.int64).to(self.device)
         di = torch.tensor(dst, dtype=torch.int64).to(self.device)
         for t in (self.s_ids, self.s_pos, self.s_ctx, self.s_state, self.s_rem, self.s_nout, self.s_seed, self.s_temp,
-                  self.s_out, self.s_bt):
+                  self.s_topk, self.s_topp, self.s_out, self.s_bt):
             t[di] = t[si]
         self.s_state[si] = -1
         self.s_bt[si] = 0

@@ -81,13 +81,13 @@ def paged_attention(q, k_cache, v_cache, block_table, q_start, ctx_len, tiles=No
 
 
 def constrained_sample(logits, row_of_slot, next_tab, dist, done_state: int, state, remaining, temperature, seed,
-                       ids, pos, ctx, nout, out_tokens) -> None:
+                       ids, pos, ctx, nout, out_tokens, topk=None, topp=None) -> None:
     if logits.is_cuda:
         _k().constrained_sample(logits, row_of_slot, next_tab, dist, done_state, state, remaining, temperature, seed,
-                                ids, pos, ctx, nout, out_tokens)
+                                ids, pos, ctx, nout, out_tokens, topk, topp)
     else:
         ref.constrained_sample(logits, row_of_slot, next_tab, dist, done_state, state, remaining, temperature, seed,
-                               ids, pos, ctx, nout, out_tokens)
+                               ids, pos, ctx, nout, out_tokens, topk, topp)
 
 
 def attention_tiles(q_lens: list[int], hq: int, hkv: int, nqt: int) -> list[tuple[int, int]]:

@@ -112,8 +112,34 @@ def paged_attention(q, k_cache, v_cache, block_table, q_start, ctx_len, tiles=No
     return out
 
 
+def ord_key(x: torch.Tensor) -> torch.Tensor:
+    """Monotone 16-bit key of the bf16 rounding of x (the kernel's top-k/top-p ranking key)."""
+    b = x.to(torch.bfloat16).view(torch.int16).to(torch.int32) & 0xFFFF
+    return torch.where(b & 0x8000 != 0, (~b) & 0xFFFF, b | 0x8000)
+
+
+def topkp_threshold(logits: torch.Tensor, legal: torch.Tensor, top_k: int, top_p: float) -> int:
+    """Smallest key kept by top-k / top-p (llama.cpp order: raw logits), ties kept; 0 = no filtering."""
+    x = logits.float()[legal]
+    if x.numel() == 0:
+        return 0
+    keys = ord_key(x)
+    thr = 0
+    if top_k > 0:
+        ks = torch.sort(keys, descending=True).values
+        thr = max(thr, int(ks[min(top_k, ks.numel()) - 1]))
+    if top_p < 1.0:
+        mass = torch.exp(x - x.max())
+        uk, inv = torch.unique(keys, return_inverse=True)          # ascending unique keys
+        km = torch.zeros(uk.numel(), dtype=torch.float64).index_add_(0, inv, mass.double())
+        cum = torch.flip(torch.cumsum(torch.flip(km, [0]), 0), [0])   # mass of keys >= uk[i]
+        ok = (cum >= top_p * float(mass.sum())).nonzero()
+        thr = max(thr, int(uk[int(ok.max())]) if ok.numel() else 0)
+    return thr
+
+
 def constrained_sample(logits, row_of_slot, next_tab, dist, done_state: int, state, remaining, temperature, seed,
-                       ids, pos, ctx, nout, out_tokens) -> None:
+                       ids, pos, ctx, nout, out_tokens, topk=None, topp=None) -> None:
     """Greedy / Gumbel-max sampling restricted by the token DFA; advances the slot state in place (host loop)."""
     n = state.numel()
     V = next_tab.shape[1]
@@ -133,6 +159,11 @@ def constrained_sample(logits, row_of_slot, next_tab, dist, done_state: int, sta
             continue
         sc = logits[row, :V].float()
         t = float(temperature[slot]) if temperature is not None else 0.0
+        tk = int(topk[slot]) if topk is not None else 0
+        tp = float(topp[slot]) if topp is not None else 1.0
+        if t > 0 and (tk > 0 or tp < 1.0):
+            thr = topkp_threshold(sc, legal, tk, tp)
+            legal = legal & (ord_key(sc) >= thr)
         if t > 0:
             g = torch.Generator(device="cpu")
             g.manual_seed((int(seed[slot]) if seed is not None else 0) * 1000003 + int(nout[slot]) * 7919 + slot)

@@ -56,6 +56,7 @@ def _worker(rank: int, cfg_dict: dict, req_q, res_q, device: str) -> None:
             ids = chat_prompt_ids(eng.tok, p.messages) if p.messages is not None else \
                 eng.tok.chat_ids(p.prompt, system=p.system, raw=p.raw)
             eng.submit(ids, fmt=p.format, num_predict=p.num_predict, temperature=p.temperature, seed=p.seed,
+                       top_k=p.top_k, top_p=p.top_p,
                        callback=finish(rid), meta={"on_tokens": tokens(rid)} if stream else None)
             try:
                 item = req_q.get_nowait()

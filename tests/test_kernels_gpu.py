@@ -355,3 +355,42 @@ def test_engine_fp8_kv_end_to_end():
     r = eng.submit(build_prompt(["[EXEC] bash -> curl", "[OPEN] curl -> /tmp/x"]), fmt=VERDICT_SCHEMA, num_predict=40)
     eng.run_until_idle()
     assert {"risk_score", "verdict", "reason"} <= set(json.loads(r.text))
+
+
+@pytest.mark.parametrize("tk,tp", [(5, 1.0), (0, 0.5), (40, 0.9), (1, 1.0)])
+def test_topk_topp_sampling_stays_in_nucleus(tk, tp):
+    """Sampled tokens must lie in the exact top-k / top-p set of the reference (keys of the bf16 logits)."""
+    from chronos import ops
+    from chronos.brain.constrain import DONE, GrammarBank
+    from chronos.brain.tokenizer import ChronosBPE
+    from chronos.ops import reference as ref
+
+    tok = ChronosBPE()
+    bank = GrammarBank(tok.token_bytes_list(), tok.stop_ids, 128256, 64, DEV)
+    g0 = bank.get(None)
+    S = 64
+    gen = torch.Generator(device=DEV).manual_seed(tk * 7 + int(tp * 10))
+    logits = (torch.randn(S, 128256, device=DEV, generator=gen) * 2).to(torch.bfloat16)
+    logits[:, 1000:1010] += 8.0  # a peaked head so top-p cuts somewhere interesting
+    i32 = dict(dtype=torch.int32, device=DEV)
+    state = torch.full((S,), g0.start, **i32)
+    rem = torch.full((S,), 50, **i32)
+    temp = torch.full((S,), 1.0, dtype=torch.float32, device=DEV)
+    seed = torch.arange(S, **i32)
+    ids, pos, ctx, nout = (torch.zeros(S, **i32) for _ in range(4))
+    out = torch.zeros(S, 4, **i32)
+    topk = torch.full((S,), tk, **i32)
+    topp = torch.full((S,), tp, dtype=torch.float32, device=DEV)
+    ops.constrained_sample(logits, None, bank.next, bank.dist, DONE, state, rem, temp, seed, ids, pos, ctx, nout,
+                           out, topk, topp)
+    legal = (bank.next[g0.start].long() >= 0).cpu()
+    legal &= bank.dist.cpu()[bank.next[g0.start].long().clamp(min=0).cpu()] <= 49
+    for s in range(S):
+        lg = logits[s].float().cpu()
+        thr = ref.topkp_threshold(lg, legal, tk, tp)
+        t = int(out[s, 0])
+        assert bool(legal[t]) and int(ref.ord_key(lg[t:t + 1])[0]) >= thr, (s, t)
+    if tk == 1:  # top-1 sampling is greedy (up to ties of the bf16 maximum, all of which are kept)
+        lgl = torch.where(legal, logits.float().cpu(), -1e30)
+        picked = lgl.gather(1, out[:, :1].long().cpu()).squeeze(1)
+        assert torch.equal(picked, lgl.max(-1).values)
