@@ -71,8 +71,9 @@ class _Base:
         raise NotImplementedError
 
     def decode(self, ids: Sequence[int]) -> str:
-        return b"".join(self.token_bytes_list()[i] for i in ids if i < len(self.token_bytes_list())).decode(
-            "utf-8", errors="replace")
+        tb = self.token_bytes_list()
+        n = len(tb)
+        return b"".join([tb[i] for i in ids if 0 <= i < n]).decode("utf-8", errors="replace")
 
     def token_bytes_list(self) -> list[bytes]:
         raise NotImplementedError
@@ -99,8 +100,27 @@ class ChronosBPE(_Base):
         self.n_bpe = self._tok.get_vocab_size()
         assert self.n_bpe < BOS_ID
         self._bytes: list[bytes] | None = None
+        import regex
+
+        # The ByteLevel pre-tokenizer splits text with the GPT-2 pattern and BPE never merges across pieces, so
+        # caching each piece's ids is exact.  Telemetry pieces (paths, comms, template words) repeat constantly:
+        # this halves the host-side tokenizer cost of a 1024-chain wave (tests/test_brain_cpu.py checks equality).
+        self._pat = regex.compile(r"""'s|'t|'re|'ve|'m|'ll|'d| ?\p{L}+| ?\p{N}+| ?[^\s\p{L}\p{N}]+|\s+(?!\S)|\s+""")
+        self._pieces: dict[str, list[int]] = {}
 
     def encode(self, text: str) -> list[int]:
+        out: list[int] = []
+        cache = self._pieces
+        for piece in self._pat.findall(text):
+            ids = cache.get(piece)
+            if ids is None:
+                ids = self._tok.encode(piece, add_special_tokens=False).ids
+                if len(cache) < 1_000_000:
+                    cache[piece] = ids
+            out += ids
+        return out
+
+    def encode_uncached(self, text: str) -> list[int]:
         return self._tok.encode(text, add_special_tokens=False).ids
 
     def encode_batch(self, texts: Sequence[str]) -> list[list[int]]:

@@ -84,6 +84,17 @@ def test_tokenizer_roundtrip_and_template(tok):
     assert len(tb) == 128256 and tb[BOS_ID] == b"" and b"".join(tb[i] for i in ids) == p.encode()
 
 
+def test_piece_cached_encoding_is_exact(tok):
+    from chronos.sensor.prompt import build_prompt
+    from chronos.sensor.replay import synthetic_chains
+
+    texts = ["\n\n" + build_prompt(c.history) for c in synthetic_chains(300, seed=21, native=False)]
+    texts += ["hello   world\n\n  x", "a\tb  \n", "naïve café 日本語 123456", "  leading", "trailing  ", "''s 're",
+              "x\n\n\n", '{"risk_score": 8, "verdict": "MALICIOUS"}']
+    for t in texts + texts:  # second pass hits the cache
+        assert tok.encode(t) == tok.encode_uncached(t)
+
+
 def test_grammar_bank_walk(tok):
     from chronos.brain.constrain import DONE, GrammarBank
     from chronos.sensor.prompt import VERDICT_SCHEMA
