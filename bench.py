@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import statistics
 import sys
@@ -39,6 +40,7 @@ def parse():
     ap.add_argument("--burst", type=int, default=8)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-prefix-cache", action="store_true")
+    ap.add_argument("--async-harvest", action="store_true")
     ap.add_argument("--device", default="cuda")
     return ap.parse_args()
 
@@ -61,7 +63,7 @@ def main():
 
     cfg = EngineConfig(model=a.model, device=str(device), max_slots=a.streams, max_model_len=512,
                        default_num_predict=a.num_predict, decode_burst=a.burst, use_graphs=not a.no_graphs,
-                       prefix_cache=not a.no_prefix_cache, seed=0)
+                       prefix_cache=not a.no_prefix_cache, async_harvest=a.async_harvest, seed=0)
     eng = Engine(cfg)
     total_steps = a.warmup + a.steps
     chains = synthetic_chains(a.streams * total_steps + a.single_stream, seed=1000 + rank)
@@ -152,7 +154,7 @@ def main():
                 "format": "verdict JSON schema (constrained decode)",
             },
             "p50_verdict_latency_ms": round(1000 * statistics.median(lats), 2),
-            "p99_verdict_latency_ms": round(1000 * sorted(lats)[int(0.99 * (len(lats) - 1))], 2),
+            "p99_verdict_latency_ms": round(1000 * sorted(lats)[max(0, math.ceil(0.99 * len(lats)) - 1)], 2),
             "single_stream_p50_latency_ms": round(1000 * statistics.median(singles), 2) if singles else None,
             "verdicts_valid": f"{oks}/{n}",
             "prompt_tokens_per_chain": round(sum(s["ptok"] for s in allst) / n, 1),

@@ -88,7 +88,12 @@ __global__ void __launch_bounds__(256) rmsnorm_kernel(const uint16_t* __restrict
 //   v  -> v_cache[blk, h, :, t % BS]        transposed    (A operand of O^T = V^T P^T, see attention.hip)
 // The cache slot is derived on device from block_table[tok_seq[t], pos / BS] so a captured decode graph needs no
 // host-side slot mapping.  cos_sin[pos, 0:64] = cos, [64:128] = sin (f32, precomputed on the host incl. Llama-3.1
-// frequency scaling).  8 threads per head, each owning dims {8i..8i+7} and {64+8i..64+8i+7}.
+// frequency scaling).
+// Thread map per token (blockIdx.x = token, blockIdx.y * 256 + threadIdx.x = g):
+//   g <  8*(Hq+Hkv):  8 threads per q/k head, each owning dims {8i..8i+7} and {64+8i..64+8i+7} (16-B loads/stores);
+//   g >= 8*(Hq+Hkv):  one wave per v head, lane l owning dims l and 64+l.  The transposed V row is 128 values each
+//                     BS*2 bytes apart: with a whole wave on consecutive dims, one store instruction covers 64 dims
+//                     in 16 cache lines (4 lanes per line, merged), instead of 64 lines with 8 threads per head.
 // ------------------------------------------------------------------------------------------------------------------
 template <bool FP8>
 __global__ void __launch_bounds__(256) rope_kv_write_kernel(
@@ -98,17 +103,18 @@ __global__ void __launch_bounds__(256) rope_kv_write_kernel(
     int block_size, int write_q, float k_inv_scale, float v_inv_scale) {
     constexpr int D = 128;
     const int t = blockIdx.x;
-    const int unit = blockIdx.y * 32 + (threadIdx.x >> 3);  // head index over [q heads | k heads | v heads]
-    const int i = threadIdx.x & 7;
+    const int g = blockIdx.y * 256 + threadIdx.x;
     const int nh = hq + 2 * hkv;
-    if (unit >= nh) return;
+    const int nrope = 8 * (hq + hkv);
+    if (g >= nrope + 64 * hkv) return;
     const int p = pos[t];
-    const uint16_t* src = qkv + ((int64_t)t * nh + unit) * D;
     const int seq = tok_seq[t];
     const int64_t blk = block_table[(int64_t)seq * bt_stride + p / block_size];
     const int off = p % block_size;
-    if (unit < hq + hkv) {
+    if (g < nrope) {
+        const int unit = g >> 3, i = g & 7;
         if (unit < hq && !write_q) return;
+        const uint16_t* src = qkv + ((int64_t)t * nh + unit) * D;
         const u16x8 a = *reinterpret_cast<const u16x8*>(src + 8 * i);
         const u16x8 b = *reinterpret_cast<const u16x8*>(src + 64 + 8 * i);
         const float* cs = cos_sin + (int64_t)p * D;
@@ -148,31 +154,19 @@ __global__ void __launch_bounds__(256) rope_kv_write_kernel(
             *reinterpret_cast<uint2*>(dst + 64 + 8 * i) = qb;
         }
     } else {
-        const int h = unit - hq - hkv;
-        const u16x8 a = *reinterpret_cast<const u16x8*>(src + 16 * i);
-        const u16x8 b = *reinterpret_cast<const u16x8*>(src + 16 * i + 8);
+        const int h = (g - nrope) >> 6, l = (g - nrope) & 63;
+        const uint16_t* src = qkv + ((int64_t)t * nh + hq + hkv + h) * D;
+        const uint16_t a = src[l], b = src[64 + l];
         const int64_t base = ((blk * hkv + h) * D) * (int64_t)block_size + off;
         if constexpr (FP8) {
             uint8_t* dst = reinterpret_cast<uint8_t*>(v_cache) + base;
-#pragma unroll
-            for (int j = 0; j < 8; j += 4) {
-                const uint32_t qa = f32x4_to_fp8x4(bf2f(a[j]) * v_inv_scale, bf2f(a[j + 1]) * v_inv_scale,
-                                                   bf2f(a[j + 2]) * v_inv_scale, bf2f(a[j + 3]) * v_inv_scale);
-                const uint32_t qb = f32x4_to_fp8x4(bf2f(b[j]) * v_inv_scale, bf2f(b[j + 1]) * v_inv_scale,
-                                                   bf2f(b[j + 2]) * v_inv_scale, bf2f(b[j + 3]) * v_inv_scale);
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    dst[(int64_t)(16 * i + j + e) * block_size] = (uint8_t)(qa >> (8 * e));
-                    dst[(int64_t)(16 * i + 8 + j + e) * block_size] = (uint8_t)(qb >> (8 * e));
-                }
-            }
+            const uint32_t q = f32x4_to_fp8x4(bf2f(a) * v_inv_scale, bf2f(b) * v_inv_scale, 0.f, 0.f);
+            dst[(int64_t)l * block_size] = (uint8_t)q;
+            dst[(int64_t)(64 + l) * block_size] = (uint8_t)(q >> 8);
         } else {
             uint16_t* dst = reinterpret_cast<uint16_t*>(v_cache) + base;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                dst[(int64_t)(16 * i + j) * block_size] = a[j];
-                dst[(int64_t)(16 * i + 8 + j) * block_size] = b[j];
-            }
+            dst[(int64_t)l * block_size] = a;
+            dst[(int64_t)(64 + l) * block_size] = b;
         }
     }
 }
@@ -230,8 +224,7 @@ void launch_rope_kv_write(const uint16_t* qkv, const int32_t* pos, const int32_t
                           int hq, int hkv, int block_size, int write_q, bool fp8, float k_scale, float v_scale,
                           hipStream_t st) {
     if (t == 0) return;
-    const int nh = hq + 2 * hkv;
-    const dim3 g(t, (nh + 31) / 32), b(256);
+    const dim3 g(t, (8 * (hq + hkv) + 64 * hkv + 255) / 256), b(256);
     if (fp8)
         hipLaunchKernelGGL(rope_kv_write_kernel<true>, g, b, 0, st, qkv, pos, tok_seq, block_table, bt_stride, cos_sin,
                            q_out, k_cache, v_cache, hq, hkv, block_size, write_q, 1.f / k_scale, 1.f / v_scale);

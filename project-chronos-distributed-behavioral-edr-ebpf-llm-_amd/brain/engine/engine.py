@@ -10,7 +10,9 @@ Replaces what Ollama + llama.cpp did for the reference (SURVEY.md §1.2 N4, §3.
 * **decode**: all slots advance together; the step (32 layers + LM head + the constrained sampler, which also
   advances ids/positions/context/DFA state on device) is captured once per power-of-two slot bucket into a hipGraph
   holding ``decode_burst`` unrolled steps, so one host call runs e.g. 8 verdict tokens for every live stream;
-* **harvest**: after each step the host reads the slot states once, detokenizes finished verdicts and frees slots.
+* **harvest**: each decode burst ends with an async copy of the slot states into pinned host memory; the host
+  harvests burst k (detokenize finished verdicts, free + compact slots) while burst k+1 already runs on the GPU, and
+  prefill steps never sync, so the host builds the next chunk while the current one computes.
 
 The reference's ``analyze_sequence`` blocked the sensor for one chain at a time (quirk Q1); here thousands of chains
 are in flight and each returns as soon as its own verdict closes.
@@ -29,7 +31,7 @@ from typing import Any, Callable, Optional
 import torch
 
 from ... import ops
-from ...models.llama import KVCache, LlamaModel, StepBatch, build_model, make_prefill_batch
+from ...models.llama import KVCache, LlamaModel, StepBatch, build_model, h2d, make_prefill_batch
 from ...parallel.tp import TPContext
 from ..constrain import DONE, GrammarBank
 from ..tokenizer import load_tokenizer
@@ -62,6 +64,7 @@ class EngineConfig:
     kv_dtype: str = "bf16"         # "bf16" or "fp8" (OCP e4m3fn, per-layer scale: half the KV bytes, 2x tokens/GPU)
     kv_scale: float = 1.0          # fp8 KV scale (stored = value / scale)
     prefill_nqt: int = 8           # 8 = flash prefill kernel (128 query rows / workgroup); 1-2 = split-K kernel
+    async_harvest: bool = False    # harvest burst k while burst k+1 runs (hides host work, delays compaction)
 
 
 @dataclass
@@ -77,6 +80,7 @@ class Request:
     top_k: int = 0                 # 0 = off
     top_p: float = 1.0             # 1.0 = off
     # runtime
+    pending_text: Optional[tuple] = None  # (prompt, system, raw) until tokenized at admission
     slot: int = -1
     blocks: list = field(default_factory=list)
     prefilled: int = 0
@@ -96,7 +100,26 @@ class Request:
 
 
 def _bucket(n: int) -> int:
-    return 1 << max(0, (n - 1).bit_length())
+    """Decode batch rows for n live slots: powers of two up to 256, then multiples of 256.  Above 256 rows a decode
+    step is GEMM-compute-bound with cost stepping at the library's 256-row M tile (896 rows cost what 1024 do, 768
+    rows 15% less: profiles/), so 256-row steps let the tail of a wave shed cost as verdicts finish instead of only
+    at each halving."""
+    if n <= 256:
+        return 1 << max(0, (n - 1).bit_length())
+    return (n + 255) // 256 * 256
+
+
+@dataclass
+class _Snapshot:
+    """Slot states copied (asynchronously) to pinned host memory at the end of a decode burst.  ``owners`` maps each
+    slot to the request that occupied it when the copy was queued: slots can be freed, refilled or compacted before
+    the snapshot is read, and those requests are matched by identity, never by slot number."""
+    n: int
+    event: Any
+    state: torch.Tensor
+    nout: torch.Tensor
+    out: torch.Tensor
+    owners: dict
 
 
 class Engine:
@@ -167,6 +190,13 @@ class Engine:
         self._graph_pool = None
         self.stats = collections.Counter()
         self._lock = threading.Lock()
+        # ---- harvest snapshots: two pinned host copies of (state, nout, out), alternated per burst ----
+        pin = self.device.type == "cuda"
+        self._snap_bufs = [tuple(torch.zeros(shape, dtype=torch.int32, pin_memory=pin)
+                                 for shape in ((S,), (S,), (S, cfg.max_out))) for _ in range(2)]
+        self._snap_i = 0
+        self._pending: Optional[_Snapshot] = None
+        self._async = cfg.async_harvest
         if self.device.type == "cuda":
             self._warmup()
 
@@ -177,42 +207,63 @@ class Engine:
                seed: int = 0, raw: bool = False, system: str | None = None,
                callback: Callable[[Request], None] | None = None, meta: dict | None = None, top_k: int = 0,
                top_p: float = 1.0) -> Request:
-        ids = prompt if isinstance(prompt, list) else self.tok.chat_ids(prompt, system=system, raw=raw)
+        """Queue a request.  A text prompt is tokenized (chat template) lazily at admission, a prefill chunk's worth
+        at a time, so host tokenization of a large wave overlaps the GPU prefill of the previous chunk."""
         n = num_predict if num_predict and num_predict > 0 else self.cfg.default_num_predict
-        n = min(n, self.cfg.max_out, self.cfg.max_model_len - len(ids))
-        req = Request(next(self._rid), ids, fmt, n, float(temperature or 0.0), int(seed or 0), callback, meta or {})
+        req = Request(next(self._rid), prompt if isinstance(prompt, list) else [], fmt, min(n, self.cfg.max_out),
+                      float(temperature or 0.0), int(seed or 0), callback, meta or {})
         req.top_k, req.top_p = int(top_k or 0), float(top_p if top_p is not None else 1.0)
         req.t_submit = time.perf_counter()
-        if n <= 0:
-            req.error = f"prompt of {len(ids)} tokens exceeds max_model_len {self.cfg.max_model_len}"
-            self._finish(req, "error")
-            return req
         try:
             req.start_state = self.bank.get(fmt).start
         except Exception as e:  # bad schema: report, never crash the engine
             req.error = f"invalid format: {e}"
             self._finish(req, "error")
             return req
-        need = self.bank.min_tokens(req.start_state)
-        if n < need:
-            req.error = f"num_predict={n} cannot fit the shortest output of this format ({need} tokens)"
-            self._finish(req, "error")
+        if not isinstance(prompt, list):
+            req.pending_text = (prompt, system, raw)
+        if not self._check_length(req):  # a text prompt's length is re-checked once it is tokenized
             return req
         with self._lock:
             self.waiting.append(req)
         return req
 
+    def _check_length(self, req: Request) -> bool:
+        """Clamp num_predict to the context left after the prompt; finish the request with an error if nothing (or
+        less than the format's shortest output) fits."""
+        ids = req.prompt_ids
+        req.num_predict = n = min(req.num_predict, self.cfg.max_model_len - len(ids))
+        if n <= 0:
+            req.error = f"prompt of {len(ids)} tokens exceeds max_model_len {self.cfg.max_model_len}"
+        elif n < self.bank.min_tokens(req.start_state):
+            need = self.bank.min_tokens(req.start_state)
+            req.error = f"num_predict={n} cannot fit the shortest output of this format ({need} tokens)"
+        if req.error:
+            self._finish(req, "error")
+            return False
+        return True
+
     def has_work(self) -> bool:
         return bool(self.waiting or self.prefilling or self.running)
 
     def step(self) -> list[Request]:
-        """One scheduling iteration: admit + prefill if anything is waiting, else one decode burst."""
+        """One scheduling iteration: admit + prefill if anything is waiting, else one decode burst.
+
+        A prefill step never syncs: its first tokens are sampled on device and a request that finishes on them is
+        harvested after the next burst.  A decode burst queues its own snapshot and (async mode) harvests the previous
+        one, which completed as soon as the GPU started on this burst."""
         self._admit()
         if self.prefilling:
             self._prefill_step()
-        elif self.running:
-            self._decode_burst()
-        return self._harvest()
+            return []
+        if self.running:
+            snap = self._decode_burst()
+            if not self._async:
+                return self._harvest(snap)
+            prev, self._pending = self._pending, snap
+            return self._harvest(prev) if prev is not None else []
+        self._pending = None
+        return []
 
     def run_until_idle(self, max_steps: int = 10**9) -> list[Request]:
         done = []
@@ -231,9 +282,19 @@ class Engine:
     # scheduling
     # ------------------------------------------------------------------------------------------------------------
     def _admit(self) -> None:
+        slots, rows = [], []
+        # admit about one prefill chunk ahead: the rest stays queued (and untokenized) while that chunk computes
+        budget = self.cfg.max_prefill_tokens - sum(len(r.prompt_ids) - r.prefilled for r in self.prefilling)
         with self._lock:
-            while self.waiting and self.free_slots:
+            while self.waiting and self.free_slots and budget > 0:
                 req = self.waiting[0]
+                if req.pending_text is not None:
+                    text, system, raw = req.pending_text
+                    req.pending_text = None
+                    req.prompt_ids = self.tok.chat_ids(text, system=system, raw=raw)
+                    if not self._check_length(req):
+                        self.waiting.popleft()
+                        continue
                 nblk = self.blocks.blocks_for(len(req.prompt_ids) + req.num_predict)
                 shared = self.blocks.lookup(req.prompt_ids)  # cached prefix blocks (already referenced)
                 if not self.blocks.can_alloc(nblk - len(shared)):
@@ -250,9 +311,12 @@ class Engine:
                 req.slot = self.free_slots.pop()
                 req.t_admit = time.perf_counter()
                 self.prefilling.append(req)
-                row = torch.zeros(self.max_blocks_per_seq, dtype=torch.int32)
-                row[:nblk] = torch.tensor(req.blocks, dtype=torch.int32)
-                self.s_bt[req.slot].copy_(row, non_blocking=True)
+                budget -= len(req.prompt_ids) - req.prefilled
+                slots.append(req.slot)
+                rows.append(req.blocks + [0] * (self.max_blocks_per_seq - nblk))
+        if slots:  # one pinned scatter for the whole admission round
+            self.s_bt[h2d(torch.tensor(slots, dtype=torch.int64), self.device)] = h2d(
+                torch.tensor(rows, dtype=torch.int32), self.device)
 
     def _prefill_step(self) -> None:
         budget = self.cfg.max_prefill_tokens
@@ -283,7 +347,7 @@ class Engine:
         # initialise the finished prompts' slots and sample their first token
         slots = torch.tensor([r.slot for r in done_reqs], dtype=torch.int64)
         plen = torch.tensor([len(r.prompt_ids) for r in done_reqs], dtype=torch.int32)
-        dv = lambda t: t.to(self.device, non_blocking=True)  # noqa: E731
+        dv = lambda t: h2d(t, self.device)  # noqa: E731
         sl = dv(slots)
         self.s_state[sl] = dv(torch.tensor([r.start_state for r in done_reqs], dtype=torch.int32))
         self.s_rem[sl] = dv(torch.tensor([r.num_predict for r in done_reqs], dtype=torch.int32))
@@ -319,7 +383,7 @@ class Engine:
     def _nsplit(self, n: int) -> int:
         return ops.pick_nsplit(n * self.model.hkv, self.cfg.max_model_len)
 
-    def _decode_burst(self) -> None:
+    def _decode_burst(self) -> _Snapshot:
         n = min(self._decode_rows(), self.cfg.max_slots)
         k = self.cfg.decode_burst
         if self.device.type == "cuda" and self.cfg.use_graphs:
@@ -332,6 +396,19 @@ class Engine:
                 self._decode_once(n, self._nsplit(n))
         self.stats["decode_steps"] += k
         self.stats["decode_row_steps"] += k * n
+        return self._snapshot(n)
+
+    def _snapshot(self, n: int) -> _Snapshot:
+        st, no, out = self._snap_bufs[self._snap_i]
+        self._snap_i ^= 1
+        st[:n].copy_(self.s_state[:n], non_blocking=True)
+        no[:n].copy_(self.s_nout[:n], non_blocking=True)
+        out[:n].copy_(self.s_out[:n], non_blocking=True)
+        ev = None
+        if self.device.type == "cuda":
+            ev = torch.cuda.Event()
+            ev.record()
+        return _Snapshot(n, ev, st, no, out, dict(self.running))
 
     def _capture(self, n: int) -> "torch.cuda.CUDAGraph":
         if self._graph_pool is None:
@@ -353,33 +430,37 @@ class Engine:
         self._decode_once(n, self._nsplit(n))
         torch.cuda.synchronize()
 
-    def _harvest(self) -> list[Request]:
-        if not self.running:
+    def _harvest(self, snap: _Snapshot) -> list[Request]:
+        if snap.event is not None:
+            snap.event.synchronize()
+        # (snapshot slot, request) for requests still running as the same object (identity, not slot number)
+        live = [(s, r) for s, r in snap.owners.items() if self.running.get(r.slot) is r]
+        if not live:
             return []
-        n = self._decode_rows()
-        st = self.s_state[:n].cpu()
-        finished = [r for s, r in self.running.items() if int(st[s]) == DONE]
-        streaming = [r for r in self.running.values() if r.meta.get("on_tokens")]
+        st = snap.state[:snap.n].tolist()
+        finished = [(s, r) for s, r in live if st[s] == DONE]
+        streaming = [(s, r) for s, r in live if r.meta.get("on_tokens")]
         if not finished and not streaming:
             return []
-        nout = self.s_nout[:n].cpu()
-        outs = self.s_out[:n].cpu()
-        for r in streaming:  # incremental tokens for stream=true clients
-            k = min(int(nout[r.slot]), self.cfg.max_out)
+        nout, outs = snap.nout, snap.out
+        for s, r in streaming:  # incremental tokens for stream=true clients
+            k = min(int(nout[s]), self.cfg.max_out)
             e = r.meta.get("emitted", 0)
             if k > e:
                 r.meta["emitted"] = k
                 try:
-                    r.meta["on_tokens"](outs[r.slot, e:k].tolist())
+                    r.meta["on_tokens"](outs[s, e:k].tolist())
                 except Exception:
                     log.exception("stream callback failed")
         if not finished:
             return []
         now = time.perf_counter()
         reset = []
-        for r in finished:
-            k = int(nout[r.slot])
-            ids = outs[r.slot, :min(k, self.cfg.max_out)].tolist()
+        done = []
+        for s, r in finished:
+            done.append(r)
+            k = int(nout[s])
+            ids = outs[s, :min(k, self.cfg.max_out)].tolist()
             stop = bool(ids) and ids[-1] in self.tok.stop_ids
             r.out_ids = ids[:-1] if stop else ids
             r.text = self.tok.decode(r.out_ids)
@@ -390,15 +471,15 @@ class Engine:
             self.free_slots.append(r.slot)
             self._finish(r, "stop" if stop else "length", timed=False)
         self.free_slots.sort(reverse=True)  # lowest slot first keeps the decode bucket small
-        idx = torch.tensor(reset, dtype=torch.int64).to(self.device)
+        idx = h2d(torch.tensor(reset, dtype=torch.int64), self.device)
         self.s_state[idx] = -1
         self.s_bt[idx] = 0
         self.s_pos[idx] = 0
         self.s_ctx[idx] = 1
-        self.stats["completed"] += len(finished)
-        self.stats["generated_tokens"] += sum(len(r.out_ids) for r in finished)
+        self.stats["completed"] += len(done)
+        self.stats["generated_tokens"] += sum(len(r.out_ids) for r in done)
         self._compact()
-        return finished
+        return done
 
     def _compact(self) -> None:
         """Move live decode rows into the lowest free slots so the decode bucket (and its captured graph) shrinks as
@@ -414,8 +495,8 @@ class Engine:
         dst = sorted(s for s in self.free_slots if s < target)[:len(movers)]
         if len(dst) < len(movers):
             return
-        si = torch.tensor(movers, dtype=torch.int64).to(self.device)
-        di = torch.tensor(dst, dtype=torch.int64).to(self.device)
+        si = h2d(torch.tensor(movers, dtype=torch.int64), self.device)
+        di = h2d(torch.tensor(dst, dtype=torch.int64), self.device)
         for t in (self.s_ids, self.s_pos, self.s_ctx, self.s_state, self.s_rem, self.s_nout, self.s_seed, self.s_temp,
                   self.s_topk, self.s_topp, self.s_out, self.s_bt):
             t[di] = t[si]

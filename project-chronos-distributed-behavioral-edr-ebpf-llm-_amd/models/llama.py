@@ -423,8 +423,18 @@ def make_prefill_batch(prompts: list[list[int]], starts: list[int], block_tables
     return to_device(sb, device)
 
 
+def h2d(t: torch.Tensor | None, device) -> torch.Tensor | None:
+    """Host->device copy that never stalls the host: a pageable-memory copy waits for the stream to drain first, a
+    pinned one (PyTorch's caching host allocator) is queued, so the host builds the next batch while the GPU runs."""
+    if t is None:
+        return None
+    if torch.device(device).type == "cuda":
+        t = t.pin_memory()
+    return t.to(device, non_blocking=True)
+
+
 def to_device(sb: StepBatch, device) -> StepBatch:
-    mv = lambda t: None if t is None else t.to(device, non_blocking=True)  # noqa: E731
+    mv = lambda t: h2d(t, device)  # noqa: E731
     return StepBatch(mv(sb.ids), mv(sb.pos), mv(sb.tok_seq), mv(sb.block_table), mv(sb.q_start), mv(sb.ctx_len),
                      mv(sb.last_idx), mv(sb.tiles), sb.ntiles, sb.nqt, sb.nsplit)
 

@@ -58,3 +58,46 @@ def test_slot_compaction_preserves_outputs():
         s = solo_eng.submit(build_prompt(c.history), fmt=VERDICT_SCHEMA, num_predict=n)
         solo_eng.run_until_idle()
         assert s.out_ids == r.out_ids
+
+
+def test_async_harvest_matches_sync_with_refill_and_streaming():
+    """Harvesting burst k while burst k+1 runs (GPU default) reads slot states one burst late, across compaction and
+    slots refilled by later submissions: outputs, stream chunks and completion must equal the synchronous engine."""
+    from chronos.brain.engine.engine import Engine, EngineConfig
+    from chronos.sensor.prompt import VERDICT_SCHEMA, build_prompt
+    from chronos.sensor.replay import synthetic_chains
+
+    chains = synthetic_chains(14, seed=9, native=False)
+    budgets = [16 + 3 * (i % 7) for i in range(14)]
+
+    def run(async_harvest):
+        eng = Engine(EngineConfig(model="tiny", device="cpu", max_slots=8, max_model_len=384, use_graphs=False,
+                                  decode_burst=3, async_harvest=async_harvest))
+        streamed = {}
+        reqs = []
+
+        def submit(i):
+            r = eng.submit(build_prompt(chains[i].history), fmt=VERDICT_SCHEMA, num_predict=budgets[i],
+                           meta={"on_tokens": lambda ids, i=i: streamed.setdefault(i, []).extend(ids)})
+            reqs.append(r)
+
+        for i in range(6):
+            submit(i)
+        nxt, steps = 6, 0
+        while eng.has_work() or nxt < len(chains):
+            eng.step()
+            steps += 1
+            if steps % 2 == 0 and nxt < len(chains):  # arrivals mid-run land in freed (possibly compacted) slots
+                submit(nxt)
+                nxt += 1
+        return reqs, streamed, eng.stats
+
+    a_reqs, a_stream, a_stats = run(True)
+    s_reqs, s_stream, _ = run(False)
+    assert a_stats["compactions"] >= 1
+    for a, s in zip(a_reqs, s_reqs):
+        assert a.done_reason == s.done_reason and a.done_reason in ("stop", "length")
+        assert a.out_ids == s.out_ids
+    for i, a in enumerate(a_reqs):
+        got = a_stream.get(i, [])
+        assert got == a.out_ids or got[:-1] == a.out_ids  # the stream may include the stop token
