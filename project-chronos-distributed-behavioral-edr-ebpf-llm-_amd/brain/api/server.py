@@ -111,7 +111,8 @@ def make_app(backend, model_name: str = "llama3", request_timeout: float | None 
 
     async def healthz(request):
         info = backend.info() if hasattr(backend, "info") else {}
-        return web.json_response({"status": "ok", "uptime_s": time.time() - started, **info})
+        ok, health = backend.health() if hasattr(backend, "health") else (True, {"status": "ok"})
+        return web.json_response({**health, "uptime_s": time.time() - started, **info}, status=200 if ok else 503)
 
     async def metrics(request):
         return web.Response(text=METRICS.render(), content_type="text/plain")
@@ -185,7 +186,15 @@ def main(argv=None) -> int:
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--fake", choices=["ok", "stall", "raise", "badjson"], default=None)
     ap.add_argument("--jsonl", default=None, help="append per-request records here")
+    ap.add_argument("--request-timeout", type=float, default=0.0,
+                    help="seconds; a slower generation answers 504 and is cancelled in the engine (0 = none)")
+    ap.add_argument("--kv-dtype", choices=["bf16", "fp8"], default="bf16")
+    ap.add_argument("--roctx", action="store_true", help="emit roctx ranges for rocprofv3 --marker-trace")
     a = ap.parse_args(argv)
+    if a.roctx:
+        from ...utils import trace
+
+        trace.enable()
     logging.basicConfig(level=logging.INFO)
     METRICS.jsonl_path = a.jsonl
     if a.fake:
@@ -194,7 +203,8 @@ def main(argv=None) -> int:
         from ..engine.engine import EngineConfig
 
         cfg = EngineConfig(model=a.model, checkpoint=a.checkpoint, tokenizer=a.tokenizer, device=a.device,
-                           max_slots=a.max_slots, max_model_len=a.max_model_len)
+                           max_slots=a.max_slots, max_model_len=a.max_model_len, kv_dtype=a.kv_dtype,
+                           request_timeout_s=a.request_timeout)
         if a.dp > 1:
             from ...parallel.router import DPRouter
 
@@ -203,5 +213,6 @@ def main(argv=None) -> int:
             from .service import EngineService
 
             backend = EngineService.from_config(cfg, a.served_name)
-    web.run_app(make_app(backend, a.served_name), host=a.host, port=a.port, access_log=None)
+    app = make_app(backend, a.served_name, a.request_timeout or None)
+    web.run_app(app, host=a.host, port=a.port, access_log=None)
     return 0

@@ -1,30 +1,45 @@
 """EngineService: runs one Engine on a dedicated scheduler thread and exposes an asyncio API to the HTTP layer.
 
 Single-owner rule: only the scheduler thread touches the engine and its device state; the HTTP event
-loop hands requests over through a queue and gets results back through ``loop.call_soon_threadsafe``.
+loop hands requests (and cancellations) over through a queue and gets results back through
+``loop.call_soon_threadsafe``.
+
+Failure detection: a watchdog thread flags the service unhealthy when one engine step runs longer
+than ``step_deadline_s`` (a hung kernel or collective); ``/healthz`` then answers 503.  A request whose HTTP caller
+gave up (server-side timeout, client disconnect) is cancelled in the engine so its slot and KV blocks are reused.
 """
 from __future__ import annotations
 
 import asyncio
+import logging
 import queue
 import threading
 import time
 from typing import Any, AsyncIterator, Optional
 
+from ...utils import trace
 from ...utils.metrics import METRICS
 from ..engine.engine import Engine, EngineConfig, Request
 from .protocol import GenerateParams, chat_prompt_ids
 
+log = logging.getLogger("chronos.service")
+
 
 class EngineService:
-    def __init__(self, engine: Engine, model_name: str = "llama3"):
+    def __init__(self, engine: Engine, model_name: str = "llama3", step_deadline_s: float = 120.0):
         self.engine = engine
         self.model_name = model_name
+        self.step_deadline_s = step_deadline_s
         self._q: "queue.Queue[tuple]" = queue.Queue()
         self._stop = threading.Event()
+        self._step_t0: Optional[float] = None  # start of the step in progress (None between steps)
+        self.stalled = False
+        self.last_error: Optional[str] = None
         self._thread = threading.Thread(target=self._loop, name="chronos-scheduler", daemon=True)
+        self._watchdog = threading.Thread(target=self._watch, name="chronos-watchdog", daemon=True)
         self.started = time.time()
         self._thread.start()
+        self._watchdog.start()
 
     @classmethod
     def from_config(cls, cfg: EngineConfig, model_name: str = "llama3") -> "EngineService":
@@ -40,26 +55,58 @@ class EngineService:
             except queue.Empty:
                 item = None
             while item is not None:
-                self._admit(item)
+                self._handle(item)
                 try:
                     item = self._q.get_nowait()
                 except queue.Empty:
                     item = None
             if eng.has_work():
-                t = time.perf_counter()
-                done = eng.step()
+                t = self._step_t0 = time.perf_counter()
+                try:
+                    with trace.range("engine.step"):
+                        done = eng.step()
+                except Exception as e:  # an engine fault fails loudly in health, never silently
+                    log.exception("engine step failed")
+                    self.last_error = f"{type(e).__name__}: {e}"
+                    self.stalled = True
+                    self._step_t0 = None
+                    continue
+                self._step_t0 = None
                 METRICS.observe_step(time.perf_counter() - t, eng)
                 for r in done:
                     METRICS.observe_request(r)
 
-    def _admit(self, item) -> None:
-        params, ids, on_done, on_tokens = item
-        self.engine.submit(ids, fmt=params.format, num_predict=params.num_predict, temperature=params.temperature,
-                           seed=params.seed, top_k=params.top_k, top_p=params.top_p, callback=on_done, meta={"on_tokens": on_tokens} if on_tokens else None)
+    def _watch(self) -> None:
+        while not self._stop.wait(min(1.0, self.step_deadline_s / 4)):
+            t0 = self._step_t0
+            if t0 is not None and time.perf_counter() - t0 > self.step_deadline_s and not self.stalled:
+                self.stalled = True
+                self.last_error = f"engine step exceeded {self.step_deadline_s:.0f}s deadline"
+                log.error("%s; stats=%s", self.last_error, dict(self.engine.stats))
+
+    def _handle(self, item) -> None:
+        kind = item[0]
+        if kind == "submit":
+            _, params, ids, on_done, on_tokens, handle = item
+            if handle.get("cancelled"):
+                return
+            handle["req"] = self.engine.submit(
+                ids, fmt=params.format, num_predict=params.num_predict, temperature=params.temperature,
+                seed=params.seed, top_k=params.top_k, top_p=params.top_p, callback=on_done,
+                meta={"on_tokens": on_tokens} if on_tokens else None)
+        elif kind == "cancel":
+            req = item[1].get("req")
+            if req is not None and not req.done_reason:
+                self.engine.cancel(req)
+
+    def _cancel(self, handle: dict) -> None:
+        handle["cancelled"] = True
+        self._q.put(("cancel", handle))
 
     def close(self) -> None:
         self._stop.set()
         self._thread.join(timeout=5)
+        self._watchdog.join(timeout=5)
 
     # ---- asyncio API -------------------------------------------------------------------------------------------
     def _ids(self, params: GenerateParams) -> list:
@@ -71,18 +118,24 @@ class EngineService:
     async def generate(self, params: GenerateParams) -> Request:
         loop = asyncio.get_running_loop()
         fut: asyncio.Future = loop.create_future()
+        handle: dict = {}
 
         def done(req: Request):
             loop.call_soon_threadsafe(lambda: fut.done() or fut.set_result(req))
 
-        self._q.put((params, self._ids(params), done, None))
-        return await fut
+        self._q.put(("submit", params, self._ids(params), done, None, handle))
+        try:
+            return await fut
+        except asyncio.CancelledError:  # caller timed out / disconnected: free the engine slot
+            self._cancel(handle)
+            raise
 
     async def generate_stream(self, params: GenerateParams) -> AsyncIterator[tuple[str, Optional[Request]]]:
         """Yields (text_delta, None) pieces, then ("", final_request)."""
         loop = asyncio.get_running_loop()
         aq: asyncio.Queue = asyncio.Queue()
         tok = self.engine.tok
+        handle: dict = {}
 
         def on_tokens(new_ids: list):
             loop.call_soon_threadsafe(aq.put_nowait, ("tok", new_ids))
@@ -90,27 +143,38 @@ class EngineService:
         def done(req: Request):
             loop.call_soon_threadsafe(aq.put_nowait, ("done", req))
 
-        self._q.put((params, self._ids(params), done, on_tokens))
+        self._q.put(("submit", params, self._ids(params), done, on_tokens, handle))
         pending = b""
-        while True:
-            kind, val = await aq.get()
-            if kind == "tok":
-                ids = [i for i in val if i not in tok.stop_ids]
-                pending += b"".join(tok.token_bytes_list()[i] for i in ids)
-                # emit only complete UTF-8 sequences
-                try:
-                    text = pending.decode("utf-8")
-                    pending = b""
-                except UnicodeDecodeError as e:
-                    text = pending[:e.start].decode("utf-8")
-                    pending = pending[e.start:]
-                if text:
-                    yield text, None
-            else:
-                if pending:
-                    yield pending.decode("utf-8", errors="replace"), None
-                yield "", val
-                return
+        finished = False
+        try:
+            while True:
+                kind, val = await aq.get()
+                if kind == "tok":
+                    ids = [i for i in val if i not in tok.stop_ids]
+                    pending += b"".join(tok.token_bytes_list()[i] for i in ids)
+                    # emit only complete UTF-8 sequences
+                    try:
+                        text = pending.decode("utf-8")
+                        pending = b""
+                    except UnicodeDecodeError as e:
+                        text = pending[:e.start].decode("utf-8")
+                        pending = pending[e.start:]
+                    if text:
+                        yield text, None
+                else:
+                    finished = True
+                    if pending:
+                        yield pending.decode("utf-8", errors="replace"), None
+                    yield "", val
+                    return
+        finally:
+            if not finished:  # the consumer stopped early (client went away)
+                self._cancel(handle)
+
+    def health(self) -> tuple[bool, dict[str, Any]]:
+        busy = self._step_t0
+        return not self.stalled, {"status": "stalled" if self.stalled else "ok", "error": self.last_error,
+                                  "step_running_s": round(time.perf_counter() - busy, 3) if busy else 0.0}
 
     def info(self) -> dict[str, Any]:
         eng = self.engine

@@ -10,9 +10,11 @@ Replaces what Ollama + llama.cpp did for the reference (SURVEY.md §1.2 N4, §3.
 * **decode**: all slots advance together; the step (32 layers + LM head + the constrained sampler, which also
   advances ids/positions/context/DFA state on device) is captured once per power-of-two slot bucket into a hipGraph
   holding ``decode_burst`` unrolled steps, so one host call runs e.g. 8 verdict tokens for every live stream;
-* **harvest**: each decode burst ends with an async copy of the slot states into pinned host memory; the host
-  harvests burst k (detokenize finished verdicts, free + compact slots) while burst k+1 already runs on the GPU, and
-  prefill steps never sync, so the host builds the next chunk while the current one computes.
+* **harvest**: each decode burst ends with a copy of the slot states into pinned host memory, which the host reads
+  to detokenize finished verdicts and free + compact slots (``async_harvest`` reads burst k while burst k+1 runs:
+  less host time on the critical path, but compaction one burst later — measured slower on the 1024-stream wave).
+  Prefill steps never sync and prompts are tokenized at admission one chunk ahead, so the host tokenizes and builds
+  chunk i+1 while the GPU computes chunk i.
 
 The reference's ``analyze_sequence`` blocked the sensor for one chain at a time (quirk Q1); here thousands of chains
 are in flight and each returns as soon as its own verdict closes.
@@ -33,6 +35,7 @@ import torch
 from ... import ops
 from ...models.llama import KVCache, LlamaModel, StepBatch, build_model, h2d, make_prefill_batch
 from ...parallel.tp import TPContext
+from ...utils import trace
 from ..constrain import DONE, GrammarBank
 from ..tokenizer import load_tokenizer
 from .block_manager import BlockManager
@@ -65,6 +68,7 @@ class EngineConfig:
     kv_scale: float = 1.0          # fp8 KV scale (stored = value / scale)
     prefill_nqt: int = 8           # 8 = flash prefill kernel (128 query rows / workgroup); 1-2 = split-K kernel
     async_harvest: bool = False    # harvest burst k while burst k+1 runs (hides host work, delays compaction)
+    request_timeout_s: float = 0.0  # >0: a request not finished this long after submit is cancelled (reason "timeout")
 
 
 @dataclass
@@ -190,6 +194,7 @@ class Engine:
         self._graph_pool = None
         self.stats = collections.Counter()
         self._lock = threading.Lock()
+        self._cancels: list[tuple[Request, str]] = []
         # ---- harvest snapshots: two pinned host copies of (state, nout, out), alternated per burst ----
         pin = self.device.type == "cuda"
         self._snap_bufs = [tuple(torch.zeros(shape, dtype=torch.int32, pin_memory=pin)
@@ -252,18 +257,74 @@ class Engine:
         A prefill step never syncs: its first tokens are sampled on device and a request that finishes on them is
         harvested after the next burst.  A decode burst queues its own snapshot and (async mode) harvests the previous
         one, which completed as soon as the GPU started on this burst."""
-        self._admit()
+        reaped = self._reap()
+        with trace.range("admit"):
+            self._admit()
         if self.prefilling:
-            self._prefill_step()
-            return []
+            with trace.range("prefill"):
+                self._prefill_step()
+            return reaped
         if self.running:
-            snap = self._decode_burst()
+            with trace.range("decode_burst"):
+                snap = self._decode_burst()
             if not self._async:
-                return self._harvest(snap)
-            prev, self._pending = self._pending, snap
-            return self._harvest(prev) if prev is not None else []
+                prev = snap
+            else:
+                prev, self._pending = self._pending, snap
+            if prev is None:
+                return reaped
+            with trace.range("harvest"):
+                return reaped + self._harvest(prev)
         self._pending = None
-        return []
+        return reaped
+
+    def cancel(self, req: Request, reason: str = "cancelled") -> None:
+        """Thread-safe: drop a request wherever it is (queued, prefilling or decoding) at the start of the next step;
+        its slot and KV blocks are freed and its callback fires with ``done_reason == reason``."""
+        with self._lock:
+            self._cancels.append((req, reason))
+
+    def _reap(self) -> list[Request]:
+        with self._lock:
+            todo, self._cancels = self._cancels, []
+        if self.cfg.request_timeout_s > 0:
+            dl = time.perf_counter() - self.cfg.request_timeout_s
+            todo += [(r, "timeout") for r in (*self.waiting, *self.prefilling, *self.running.values())
+                     if r.t_submit < dl]
+        out, reset = [], []
+        for req, reason in todo:
+            if req.done_reason:
+                continue  # already finished (or reaped twice)
+            if req in self.prefilling:
+                # Its prompt blocks are published in the prefix cache and may already be shared by a later request
+                # that relies on this prefill computing them: finish the prefill, then drop it (_prefill_step).
+                req.meta["cancel_reason"] = reason
+                continue
+            if self.running.get(req.slot) is req:
+                del self.running[req.slot]
+            else:
+                with self._lock:
+                    try:
+                        self.waiting.remove(req)
+                    except ValueError:
+                        continue  # not known to this engine
+            if req.slot >= 0:
+                self.blocks.release(req.blocks)
+                reset.append(req.slot)
+                self.free_slots.append(req.slot)
+                req.slot = -1
+            req.error = f"request {reason}"
+            self.stats[reason] += 1
+            self._finish(req, reason)
+            out.append(req)
+        if reset:
+            self.free_slots.sort(reverse=True)
+            idx = h2d(torch.tensor(reset, dtype=torch.int64), self.device)
+            self.s_state[idx] = -1
+            self.s_bt[idx] = 0
+            self.s_pos[idx] = 0
+            self.s_ctx[idx] = 1
+        return out
 
     def run_until_idle(self, max_steps: int = 10**9) -> list[Request]:
         done = []
@@ -368,6 +429,8 @@ class Engine:
             r.t_first = now
             self.prefilling.remove(r)
             self.running[r.slot] = r
+            if "cancel_reason" in r.meta:  # cancelled mid-prefill: its blocks are computed now, drop it next step
+                self.cancel(r, r.meta["cancel_reason"])
 
     def _decode_rows(self) -> int:
         return _bucket(max(self.running) + 1) if self.running else 0

@@ -41,6 +41,7 @@ def _worker(rank: int, cfg_dict: dict, req_q, res_q, device: str) -> None:
     def tokens(rid):
         return lambda ids: res_q.put(("tok", rid, ids))
 
+    live: dict = {}  # rid -> Request, for cancellations
     stop = False
     while not stop:
         try:
@@ -51,19 +52,26 @@ def _worker(rank: int, cfg_dict: dict, req_q, res_q, device: str) -> None:
             if item == "stop":
                 stop = True
                 break
+            if item[0] == "cancel":
+                r = live.pop(item[1], None)
+                if r is not None and not r.done_reason:
+                    eng.cancel(r)
+                item = None if req_q.empty() else req_q.get_nowait()
+                continue
             rid, pd, stream = item
             p = GenerateParams(**pd)
             ids = chat_prompt_ids(eng.tok, p.messages) if p.messages is not None else \
                 eng.tok.chat_ids(p.prompt, system=p.system, raw=p.raw)
-            eng.submit(ids, fmt=p.format, num_predict=p.num_predict, temperature=p.temperature, seed=p.seed,
-                       top_k=p.top_k, top_p=p.top_p,
-                       callback=finish(rid), meta={"on_tokens": tokens(rid)} if stream else None)
+            live[rid] = eng.submit(ids, fmt=p.format, num_predict=p.num_predict, temperature=p.temperature,
+                                   seed=p.seed, top_k=p.top_k, top_p=p.top_p, callback=finish(rid),
+                                   meta={"rid": rid, **({"on_tokens": tokens(rid)} if stream else {})})
             try:
                 item = req_q.get_nowait()
             except queue.Empty:
                 item = None
         if eng.has_work():
-            eng.step()
+            for r in eng.step():
+                live.pop(r.meta.get("rid"), None)
 
 
 class DPRouter:
@@ -107,7 +115,7 @@ class DPRouter:
             loop, sink, _ = w
             loop.call_soon_threadsafe(sink, kind, val)
 
-    def _dispatch(self, params, stream: bool, sink) -> None:
+    def _dispatch(self, params, stream: bool, sink) -> tuple[int, int]:
         loop = asyncio.get_running_loop()
         with self._lock:
             r = min(range(self.n), key=lambda i: self.outstanding[i])
@@ -115,6 +123,13 @@ class DPRouter:
             rid = next(self._rid)
             self._waiters[rid] = (loop, sink, r)
         self._reqs[r].put((rid, asdict(params), stream))
+        return rid, r
+
+    def _cancel(self, rid: int, r: int) -> None:
+        with self._lock:
+            if rid not in self._waiters:
+                return  # already finished
+        self._reqs[r].put(("cancel", rid))
 
     @staticmethod
     def _result(val: dict) -> SimpleNamespace:
@@ -130,25 +145,39 @@ class DPRouter:
             if kind == "done" and not fut.done():
                 fut.set_result(self._result(val))
 
-        self._dispatch(params, False, sink)
-        return await fut
+        rid, r = self._dispatch(params, False, sink)
+        try:
+            return await fut
+        except asyncio.CancelledError:  # HTTP timeout / disconnect: free the replica's slot
+            self._cancel(rid, r)
+            raise
 
     async def generate_stream(self, params) -> AsyncIterator[tuple[str, Optional[object]]]:
         aq: asyncio.Queue = asyncio.Queue()
-        self._dispatch(params, True, lambda kind, val: aq.put_nowait((kind, val)))
+        rid, r = self._dispatch(params, True, lambda kind, val: aq.put_nowait((kind, val)))
         from ..brain.tokenizer import load_tokenizer
 
         tok = getattr(self, "_tok", None) or load_tokenizer(None)
         self._tok = tok
-        while True:
-            kind, val = await aq.get()
-            if kind == "tok":
-                text = tok.decode([i for i in val if i not in tok.stop_ids])
-                if text:
-                    yield text, None
-            else:
-                yield "", self._result(val)
-                return
+        finished = False
+        try:
+            while True:
+                kind, val = await aq.get()
+                if kind == "tok":
+                    text = tok.decode([i for i in val if i not in tok.stop_ids])
+                    if text:
+                        yield text, None
+                else:
+                    finished = True
+                    yield "", self._result(val)
+                    return
+        finally:
+            if not finished:
+                self._cancel(rid, r)
+
+    def health(self) -> tuple[bool, dict]:
+        dead = [i for i, p in enumerate(self._procs) if not p.is_alive()]
+        return not dead, {"status": "replica down" if dead else "ok", "dead_replicas": dead}
 
     def info(self) -> dict:
         return {"engines": self.n, "outstanding": list(self.outstanding)}

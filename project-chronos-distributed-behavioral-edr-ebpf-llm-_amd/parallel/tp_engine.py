@@ -10,12 +10,15 @@ SAME scheduler, in lockstep:
 * logits are all-gathered (vocab-parallel LM head), so the fused constrained sampler computes the same tokens and
   advances the same device state on every rank — no token broadcast, and the decode burst stays one captured graph
   per rank with the RCCL all-reduces inside it;
-* finished requests are reported by the leader; followers just retire them.
+* finished requests are reported by the leader; followers just retire them;
+* cancellations and request deadlines are decided by the leader alone and broadcast as (tag, reason) with the
+  step's submissions — a rank-local clock check would let ranks drop different requests and fall out of lockstep.
 """
 from __future__ import annotations
 
 import queue
 import threading
+import time
 from dataclasses import dataclass, field
 from typing import Any, Callable, Optional
 
@@ -38,17 +41,23 @@ class _Sub:
 @dataclass
 class _Msg:
     subs: list = field(default_factory=list)
+    cancels: list = field(default_factory=list)  # (tag, reason)
     stop: bool = False
 
 
 class TPEngine:
     def __init__(self, cfg: EngineConfig, tp: TPContext, ctrl_group=None):
+        from dataclasses import replace
+
         self.tp = tp
         self.ctrl = ctrl_group  # gloo group spanning the TP ranks (host-side control plane)
-        self.engine = Engine(cfg, tp=tp)
+        self.timeout_s = cfg.request_timeout_s  # enforced by the leader only (module docstring)
+        self.engine = Engine(replace(cfg, request_timeout_s=0.0), tp=tp)
         self.leader = tp.rank == 0
         self._inbox: "queue.Queue[_Sub]" = queue.Queue()
+        self._cancel_inbox: "queue.Queue[tuple[int, str]]" = queue.Queue()
         self._callbacks: dict[int, Callable[[Request], None]] = {}
+        self._reqs: dict[int, Request] = {}  # tag -> live request (every rank)
         self._tag = 0
         self._lock = threading.Lock()
 
@@ -65,6 +74,10 @@ class TPEngine:
         self._inbox.put(_Sub(ids, fmt, num_predict, temperature, seed, tag))
         return tag
 
+    def cancel(self, tag: int, reason: str = "cancelled") -> None:
+        assert self.leader, "cancellations enter through TP rank 0"
+        self._cancel_inbox.put((tag, reason))
+
     def _exchange(self, stop: bool = False) -> _Msg:
         msg = _Msg()
         if self.leader:
@@ -73,6 +86,14 @@ class TPEngine:
                     msg.subs.append(self._inbox.get_nowait())
                 except queue.Empty:
                     break
+            while True:
+                try:
+                    msg.cancels.append(self._cancel_inbox.get_nowait())
+                except queue.Empty:
+                    break
+            if self.timeout_s > 0:
+                dl = time.perf_counter() - self.timeout_s
+                msg.cancels += [(t, "timeout") for t, r in self._reqs.items() if r.t_submit < dl]
             msg.stop = stop
         if self.tp.world > 1:
             box = [msg]
@@ -86,9 +107,17 @@ class TPEngine:
         msg = self._exchange(stop)
         for s in msg.subs:
             cb = self._callbacks.pop(s.tag, None) if self.leader else None
-            self.engine.submit(s.ids, fmt=s.fmt, num_predict=s.num_predict, temperature=s.temperature, seed=s.seed,
-                               callback=cb, meta={"tag": s.tag})
+            r = self.engine.submit(s.ids, fmt=s.fmt, num_predict=s.num_predict, temperature=s.temperature,
+                                   seed=s.seed, callback=cb, meta={"tag": s.tag})
+            if not r.done_reason:
+                self._reqs[s.tag] = r
+        for tag, reason in msg.cancels:
+            r = self._reqs.get(tag)
+            if r is not None:
+                self.engine.cancel(r, reason)
         done = self.engine.step() if self.engine.has_work() else []
+        for r in done:
+            self._reqs.pop(r.meta.get("tag"), None)
         return done, msg.stop
 
     def run_until_idle(self) -> list[Request]:

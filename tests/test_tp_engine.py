@@ -41,12 +41,16 @@ def _worker(rank, world, port, q):
         results = {}
         for i, c in enumerate(CHAINS):
             eng.submit(build_prompt(c), fmt=VERDICT_SCHEMA, num_predict=40,
-                       callback=lambda r, i=i: results.__setitem__(i, (r.out_ids, r.text)))
+                       callback=lambda r, i=i: results.__setitem__(i, (r.out_ids, r.text, r.done_reason)))
+        # a cancellation is decided by the leader and applied on every rank in the same step
+        tag = eng.submit(build_prompt(CHAINS[0]), fmt=VERDICT_SCHEMA, num_predict=40,
+                         callback=lambda r: results.__setitem__(3, (r.out_ids, r.text, r.done_reason)))
+        eng.cancel(tag)
         eng.run_until_idle()
         q.put(("leader", results))
     else:
         eng.follower_loop()
-        q.put(("follower", {s: list(r) for s, r in enumerate(eng.engine.stats.items())}))
+        q.put(("follower", dict(eng.engine.stats)))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -71,10 +75,12 @@ def test_tp2_engine_lockstep_matches_tp1():
     for p in ps:
         p.join(timeout=60)
     res = got["leader"]
-    assert sorted(res) == [0, 1, 2]
+    assert sorted(res) == [0, 1, 2, 3]
+    assert res[3][2] == "cancelled" and got["follower"]["cancelled"] == 1
+    assert got["follower"]["completed"] == 3
     agree = 0
     for i, r in enumerate(reqs):
-        ids, text = res[i]
+        ids, text, _ = res[i]
         assert set(json.loads(text)) == {"risk_score", "verdict", "reason"}
         # same model, different summation order across the TP shards: greedy paths agree on the prefix at least
         n = min(len(ids), len(r.out_ids))
