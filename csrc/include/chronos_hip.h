@@ -83,3 +83,10 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 }
 
 }  // namespace chronos
+
+namespace chronos {
+// Host-side tuning knobs (defined in bindings.cpp): value set through torch.ops.chronos.set_knob(name, v), else the
+// environment variable CHRONOS_<NAME>, else `dflt`.  Used for in-process A/B of kernel variants
+// (cdna_hip_programming.md §5.4 rule 24: interleave variants in ONE process).
+int knob(const char* name, int dflt);
+}  // namespace chronos

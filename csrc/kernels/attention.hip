@@ -283,6 +283,181 @@ __global__ void __launch_bounds__(256) paged_attn_combine_kernel(
     }
 }
 
+// ------------------------------------------------------------------------------------------------------------------
+// Decode attention for short/medium contexts (no kv split): ONE WAVE per (sequence, kv head) walks the whole context
+// in 32-token steps with the next step's K/V already in flight (two register sets), so there is no LDS merge, no
+// workgroup barrier and no partial output.  The sequence's block-table entries are fetched 64 at a time into one
+// VGPR (lane i = entry i of the window) and read with a shuffle, instead of a dependent global load per 16 tokens.
+// With ~100-200-token verdict contexts the split-over-waves kernel above spent most of its time in those fixed
+// costs (one 32-token step per wave, then merge); this form is bound by the K/V bytes.  Same MFMA mapping and the
+// same per-step arithmetic order as paged_attn_kernel<1>.
+// ------------------------------------------------------------------------------------------------------------------
+template <bool FP8, bool PF>
+__global__ void __launch_bounds__(256) paged_decode_kernel(
+    const uint16_t* __restrict__ q, const void* __restrict__ kcv, const void* __restrict__ vcv,
+    const int32_t* __restrict__ block_table, int bt_stride, const int32_t* __restrict__ ctx_len,
+    uint16_t* __restrict__ out, int nitems, int hq, int hkv, float scale_log2, float k_scale, float v_scale) {
+    constexpr int block_size = 16;  // the engine's page size; compile-time so every K/V address is base + immediate
+    const int lane = threadIdx.x & 63;
+    const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (item >= nitems) return;  // whole wave; the kernel has no workgroup-level synchronisation
+    const uint16_t* kc = reinterpret_cast<const uint16_t*>(kcv);
+    const uint16_t* vc = reinterpret_cast<const uint16_t*>(vcv);
+    const uint8_t* kc8 = reinterpret_cast<const uint8_t*>(kcv);
+    const uint8_t* vc8 = reinterpret_cast<const uint8_t*>(vcv);
+    const int seq = item / hkv, h = item - seq * hkv;
+    const int r = lane & 15, h4 = lane >> 4, G = hq / hkv;
+    const int ctx = ctx_len[seq];
+    const int32_t* bt = block_table + (int64_t)seq * bt_stride;
+    const int nblk = (ctx + block_size - 1) / block_size;
+    int win = 0;
+    int btv = lane < nblk ? bt[lane] : 0;
+
+    bf16x8 qf[4];
+    {
+        const bool valid = r < G;
+        const uint16_t* qp = q + ((int64_t)seq * hq + h * G + (valid ? r : 0)) * kD + 8 * h4;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            bf16x8 v = *reinterpret_cast<const bf16x8*>(qp + 32 * c);
+            if (!valid) v = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+            qf[c] = v;
+        }
+    }
+
+    auto load = [&](int t0, bf16x8 (&kf)[2][4], bf16x4 (&vf)[2][8]) {
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            const int tg = t0 + 16 * g;
+            if (tg < ctx) {
+                const int bi = tg / block_size;
+                while (bi >= win + 64) {  // wave-uniform: next window of 64 block-table entries
+                    win += 64;
+                    btv = win + lane < nblk ? bt[win + lane] : 0;
+                }
+                const int64_t blk = __shfl(btv, bi - win, 64);
+                const int off = tg - bi * block_size;
+                const int64_t koff = (((blk * hkv + h) * block_size) + off + r) * kD + 8 * h4;
+                const int64_t voff = ((blk * hkv + h) * kD) * (int64_t)block_size + off + 4 * h4;
+                if constexpr (FP8) {
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        const uint2 v = *reinterpret_cast<const uint2*>(kc8 + koff + 32 * c);
+                        kf[g][c] = fp8x8_to_bf16x8(v.x, v.y, k_scale);
+                    }
+#pragma unroll
+                    for (int dt = 0; dt < 8; ++dt)
+                        vf[g][dt] = fp8x4_to_bf16x4(
+                            *reinterpret_cast<const uint32_t*>(vc8 + voff + (int64_t)(dt * 16 + r) * block_size), v_scale);
+                } else {
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) kf[g][c] = *reinterpret_cast<const bf16x8*>(kc + koff + 32 * c);
+#pragma unroll
+                    for (int dt = 0; dt < 8; ++dt)
+                        vf[g][dt] = *reinterpret_cast<const bf16x4*>(vc + voff + (int64_t)(dt * 16 + r) * block_size);
+                }
+            } else {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) kf[g][c] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+                for (int dt = 0; dt < 8; ++dt) vf[g][dt] = bf16x4{0, 0, 0, 0};
+            }
+        }
+    };
+
+    float m = -1e30f, lsum = 0.f;
+    f32x4 o[8];
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto step = [&](int t0, bf16x8 (&kf)[2][4], bf16x4 (&vf)[2][8]) {
+        if (t0 + 32 > ctx) {  // partial step: zero V of keys past the end (uniform branch)
+#pragma unroll
+            for (int g = 0; g < 2; ++g)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (t0 + 16 * g + 4 * h4 + i >= ctx)
+#pragma unroll
+                        for (int dt = 0; dt < 8; ++dt) vf[g][dt][i] = (__bf16)0.f;
+        }
+        f32x4 s[2];
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[g][c], qf[c], acc, 0, 0, 0);
+            s[g] = acc;
+        }
+        float mx = -INFINITY;
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float v = s[g][i] * scale_log2;
+                if (t0 + 16 * g + 4 * h4 + i >= ctx) v = -INFINITY;
+                s[g][i] = v;
+                mx = fmaxf(mx, v);
+            }
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float mnew = fmaxf(m, mx);
+        const float alpha = exp2f(m - mnew);
+        m = mnew;
+        float ps = 0.f;
+        bf16x8 pf;
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float p = exp2f(s[g][i] - mnew);
+                ps += p;
+                pf[4 * g + i] = (__bf16)p;
+            }
+        lsum = lsum * alpha + ps;
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) {
+            o[dt] *= alpha;
+            const bf16x8 va = __builtin_shufflevector(vf[0][dt], vf[1][dt], 0, 1, 2, 3, 4, 5, 6, 7);
+            o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pf, o[dt], 0, 0, 0);
+        }
+    };
+
+    if constexpr (PF) {  // next step's K/V in flight while this one computes (two register sets, 1 wave/SIMD)
+        bf16x8 kA[2][4], kB[2][4];
+        bf16x4 vA[2][8], vB[2][8];
+        load(0, kA, vA);
+        for (int t0 = 0; t0 < ctx; t0 += 64) {
+            if (t0 + 32 < ctx) load(t0 + 32, kB, vB);
+            step(t0, kA, vA);
+            if (t0 + 32 >= ctx) break;
+            if (t0 + 64 < ctx) load(t0 + 64, kA, vA);
+            step(t0 + 32, kB, vB);
+        }
+    } else {  // one register set: latency hidden by occupancy instead (3 waves/SIMD)
+        bf16x8 kA[2][4];
+        bf16x4 vA[2][8];
+        for (int t0 = 0; t0 < ctx; t0 += 32) {
+            load(t0, kA, vA);
+            step(t0, kA, vA);
+        }
+    }
+
+    float lt = lsum;
+    lt += __shfl_xor(lt, 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    if (r < G) {
+        const float inv = lt > 0.f ? 1.f / lt : 0.f;
+        uint16_t* op = out + ((int64_t)seq * hq + h * G + r) * kD + 4 * h4;
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) {
+            u16x4 ov;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) ov[i] = f2bf(o[dt][i] * inv);
+            *reinterpret_cast<u16x4*>(op + 16 * dt) = ov;
+        }
+    }
+}
+
 size_t paged_attn_smem(int nqt) { return (size_t)(8 * nqt * 16 + 4 * nqt * 16 * kOStride) * sizeof(float); }
 
 void launch_paged_attn(const uint16_t* q, const void* kc, const void* vc, const int32_t* block_table, int bt_stride,
@@ -291,6 +466,25 @@ void launch_paged_attn(const uint16_t* q, const void* kc, const void* vc, const 
                        float scale, bool fp8, float k_scale, float v_scale, hipStream_t st) {
     if (ntiles == 0) return;
     const float scale_log2 = scale * 1.4426950408889634f;
+    // decode without a kv split and enough (seq, kv head) items to fill the chip one wave each (>= 2048 waves:
+    // 8 per CU); fewer items keep the split-over-waves form (profiles/r1_attn_decode.json: B=64 x 1k ctx is 1.5x
+    // faster there, B >= 256 at 128-512 ctx 1.0-1.3x slower)
+    const int nitems = ntiles * hkv;
+    if (tiles == nullptr && nqt == 1 && nsplit == 1 && hq / hkv <= 16 && block_size == 16 && nitems >= 2048) {
+        if (knob("decode_attn_legacy", 0)) goto legacy;  // A/B against the split-over-waves kernel
+        const int pf = knob("decode_pf", 0);
+#define PD_LAUNCH(F, P)                                                                                         \
+    hipLaunchKernelGGL((paged_decode_kernel<F, P>), dim3((nitems + 3) / 4), dim3(256), 0, st, q, kc, vc, block_table, \
+                       bt_stride, ctx_len, out, nitems, hq, hkv, scale_log2, k_scale, v_scale)
+        if (fp8) {
+            if (pf) PD_LAUNCH(true, true); else PD_LAUNCH(true, false);
+        } else {
+            if (pf) PD_LAUNCH(false, true); else PD_LAUNCH(false, false);
+        }
+#undef PD_LAUNCH
+        return;
+    }
+legacy:
     const dim3 grid(ntiles, hkv, nsplit), block(256);
     const size_t sh = paged_attn_smem(nqt);
 #define PA_LAUNCH(N, F)                                                                                         \

@@ -11,6 +11,10 @@
 
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdlib>
+#include <mutex>
+#include <string>
+#include <unordered_map>
 
 namespace chronos {
 void launch_embedding(const int32_t*, const uint16_t*, uint16_t*, int, int, int64_t, int64_t, hipStream_t);
@@ -26,9 +30,29 @@ void launch_constrained_sample(const void*, bool, int64_t, const int32_t*, int, 
                                int, int32_t*, int32_t*, const float*, const int32_t*, const int32_t*, const float*,
                                int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, int, hipStream_t);
 void launch_gemv(const uint16_t*, int, int, const uint16_t*, int, uint16_t*, bool, hipStream_t);
+void launch_gemm(const uint16_t*, const uint16_t*, uint16_t*, int, int, int, bool, int, hipStream_t);
 void launch_attn_prefill(const uint16_t*, const void*, const void*, const int32_t*, int, const int32_t*,
                          const int32_t*, const int32_t*, int, uint16_t*, int, int, int, float, bool, float, float,
                          hipStream_t);
+}  // namespace chronos
+
+namespace chronos {
+namespace {
+std::mutex g_knob_mu;
+std::unordered_map<std::string, int> g_knobs;
+}  // namespace
+
+int knob(const char* name, int dflt) {
+    std::lock_guard<std::mutex> lk(g_knob_mu);
+    auto it = g_knobs.find(name);
+    if (it != g_knobs.end()) return it->second;
+    std::string env = "CHRONOS_";
+    for (const char* c = name; *c; ++c) env += (char)toupper(*c);
+    const char* e = getenv(env.c_str());
+    const int v = e ? atoi(e) : dflt;
+    g_knobs[name] = v;
+    return v;
+}
 }  // namespace chronos
 
 namespace {
@@ -258,6 +282,27 @@ Tensor gemv(const Tensor& x, const Tensor& w, bool swiglu) {
     return y;
 }
 
+// y = x @ w.T on MFMA (gemm.hip); swiglu as gemv.  stages = depth of the LDS-DMA ring (2..4)
+Tensor gemm(const Tensor& x, const Tensor& w, bool swiglu, int64_t stages) {
+    chk_bf16(x, "x");
+    chk_bf16(w, "w");
+    const int64_t K = x.size(-1), M = x.numel() / K, N = w.size(0);
+    CHK(w.dim() == 2 && w.size(1) == K, "gemm: w must be [N, K]");
+    CHK(K % 64 == 0, "gemm: K % 64 == 0");
+    CHK(N % 128 == 0, "gemm: N % 128 == 0");
+    CHK(M < (1LL << 31) / 128 && N * K < (1LL << 40), "gemm: size");
+    CHK(stages >= 2 && stages <= 4, "gemm: stages in [2, 4]");
+    c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+    auto y = at::empty({M, swiglu ? N / 2 : N}, x.options());
+    chronos::launch_gemm(bf(x), bf(w), bfm(y), (int)M, (int)N, (int)K, swiglu, (int)stages, cur_stream());
+    return y;
+}
+
+void set_knob(const std::string& name, int64_t value) {
+    std::lock_guard<std::mutex> lk(chronos::g_knob_mu);
+    chronos::g_knobs[name] = (int)value;
+}
+
 }  // namespace
 
 TORCH_LIBRARY(chronos, m) {
@@ -269,6 +314,8 @@ TORCH_LIBRARY(chronos, m) {
           "float k_scale=1.0, float v_scale=1.0) -> ()");
     m.def("silu_mul(Tensor gate_up) -> Tensor");
     m.def("gemv(Tensor x, Tensor w, bool swiglu) -> Tensor");
+    m.def("gemm(Tensor x, Tensor w, bool swiglu, int stages=3) -> Tensor");
+    m.def("set_knob(str name, int value) -> ()", &set_knob);
     m.def("paged_attention(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_table, Tensor q_start, "
           "Tensor ctx_len, Tensor? tiles, int ntiles, int nqt, int nsplit, float scale, float k_scale=1.0, "
           "float v_scale=1.0) -> Tensor");
@@ -284,6 +331,7 @@ TORCH_LIBRARY_IMPL(chronos, CUDA, m) {
     m.impl("rope_kv_write", &rope_kv_write);
     m.impl("silu_mul", &silu_mul);
     m.impl("gemv", &gemv);
+    m.impl("gemm", &gemm);
     m.impl("paged_attention", &paged_attention);
     m.impl("constrained_sample", &constrained_sample);
 }

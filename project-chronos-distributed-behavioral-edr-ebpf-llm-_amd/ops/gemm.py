@@ -1,9 +1,15 @@
 """Projection GEMMs.
 
-``linear(x, w)`` computes ``x @ w.T`` for weights stored [out, in] (HF layout).  Plain projection GEMMs go to the
-vendor library (hipBLASLt via torch.matmul) — the task's rule for "plain library GEMMs"; the fused / skinny shapes
-that a library does not serve well get hand-written MFMA kernels registered in ``_custom`` (see csrc/kernels/gemm*.hip)
-and are selected per shape by :func:`linear`.
+``linear(x, w)`` computes ``x @ w.T`` for weights stored [out, in] (HF layout); ``gate_up_silu`` is the fused K8+K9.
+Routing is by measured shape (profiles/r1_gemm_vs_hipblaslt.json, cold weights, one MI355X):
+
+* M <= 2 (single-stream decode): the hand-written GEMV (csrc/kernels/gemv.hip), 1 KiB row-contiguous weight
+  streaming — beats hipBLASLt on every decode shape;
+* gate_up at 3 <= M <= 128: the MFMA GEMM with the fused SwiGLU epilogue (csrc/kernels/gemm.hip) — 1.05-1.24x over
+  hipBLASLt + the separate silu_mul pass, which it removes;
+* everything else: hipBLASLt via torch.matmul (the "plain library GEMM" rule).  The hand-written 128x128-tile MFMA
+  GEMM loses there: one tile per CU is bound by the per-CU load path (~0.7 us per 64-deep K-step), the same wall
+  hipBLASLt's 128x128 tiles hit, and it has no answer to the small-grid shapes (N = 4096 at M <= 128).
 """
 from __future__ import annotations
 
@@ -11,7 +17,7 @@ from typing import Callable, Optional
 
 import torch
 
-# (M, N, K) -> bool predicate + kernel; filled by the HIP GEMM module once it is loaded
+# (M, N, K) -> bool predicate + kernel; extension point for further shape-specialised kernels
 _custom: list[tuple[Callable[[int, int, int], bool], Callable[[torch.Tensor, torch.Tensor], torch.Tensor]]] = []
 
 
@@ -27,6 +33,11 @@ def gemv_ok(m: int, n: int, k: int, swiglu: bool = False) -> bool:
     return m == 1 or (m == 2 and n <= 32768)
 
 
+def mfma_swiglu_ok(m: int, n: int, k: int) -> bool:
+    """Fused gate_up + SwiGLU on the MFMA GEMM: the measured winning range (3 <= M <= 128)."""
+    return 3 <= m <= 128 and k % 64 == 0 and n % 128 == 0
+
+
 def _gemv(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False) -> torch.Tensor:
     from . import _k
 
@@ -35,12 +46,24 @@ def _gemv(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False) -> torch.Tenso
     return y.view(*x.shape[:-1], y.shape[-1])
 
 
+def mfma_gemm(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False, stages: int = 3) -> torch.Tensor:
+    from . import _k
+
+    k = x.shape[-1]
+    y = _k().gemm(x.reshape(-1, k), w, swiglu, stages)
+    return y.view(*x.shape[:-1], y.shape[-1])
+
+
 def gate_up_silu(x: torch.Tensor, w_gu: torch.Tensor) -> torch.Tensor:
-    """silu(x @ gate.T) * (x @ up.T) with w_gu = [gate; up].  Decode: one fused GEMV launch; else GEMM + silu_mul."""
+    """silu(x @ gate.T) * (x @ up.T) with w_gu = [gate; up]: one fused launch for decode batches, else GEMM + silu_mul."""
     from . import silu_mul
 
-    if x.is_cuda and gemv_ok(x.numel() // x.shape[-1], w_gu.shape[0], x.shape[-1], swiglu=True):
-        return _gemv(x, w_gu, True)
+    if x.is_cuda:
+        m, n, k = x.numel() // x.shape[-1], w_gu.shape[0], x.shape[-1]
+        if gemv_ok(m, n, k, swiglu=True):
+            return _gemv(x, w_gu, True)
+        if mfma_swiglu_ok(m, n, k):
+            return mfma_gemm(x, w_gu, True)
     return silu_mul(linear(x, w_gu))
 
 

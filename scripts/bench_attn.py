@@ -1,0 +1,83 @@
+"""Decode attention variants A/B'd in one process (torch.ops.chronos.set_knob), 8B shapes, random data:
+legacy split-over-waves kernel vs the one-wave-per-(seq, kv head) kernel with / without register prefetch.
+Reports time and logical KV bytes / time.   python scripts/bench_attn.py [--out gpurun_out/attn.json]"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def timeit(fn, iters=20, rounds=5):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    res = []
+    for _ in range(rounds):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(iters):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        res.append(s.elapsed_time(e) / iters * 1e3)
+    return statistics.median(res)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    from chronos import ops
+
+    ops.load()
+    C = torch.ops.chronos
+    dev = "cuda"
+    out = []
+    variants = {"legacy": dict(decode_attn_legacy=1, decode_pf=0), "wave": dict(decode_attn_legacy=0, decode_pf=0),
+                "wave_pf": dict(decode_attn_legacy=0, decode_pf=1)}
+    for B, ctx, fp8 in ((1024, 128, False), (1024, 200, False), (256, 160, False), (1024, 512, False),
+                        (64, 1024, False), (1024, 128, True)):
+        hq, hkv, bs = 32, 8, 16
+        nbs = (ctx + bs - 1) // bs
+        nb = B * nbs + 1
+        perm = torch.randperm(B * nbs, device=dev).to(torch.int32) + 1  # scattered pages, like a live cache
+        bt = perm.view(B, nbs)
+        if fp8:
+            k = torch.randint(0, 120, (nb, hkv, bs, 128), device=dev, dtype=torch.uint8)
+            v = torch.randint(0, 120, (nb, hkv, 128, bs), device=dev, dtype=torch.uint8)
+        else:
+            k = torch.randn(nb, hkv, bs, 128, device=dev).to(torch.bfloat16)
+            v = torch.randn(nb, hkv, 128, bs, device=dev).to(torch.bfloat16)
+        q = torch.randn(B, hq, 128, device=dev).to(torch.bfloat16)
+        qs = torch.arange(B + 1, device=dev, dtype=torch.int32)
+        cl = torch.randint(ctx // 2, ctx + 1, (B,), device=dev, dtype=torch.int32)
+        ns = ops.pick_nsplit(B * hkv, ctx)
+        res = {}
+        outs = {}
+        for name, kn in variants.items():
+            for kk, vv in kn.items():
+                C.set_knob(kk, vv)
+            fn = lambda: ops.paged_attention(q, k, v, bt, qs, cl, None, B, 1, ns)  # noqa: E731
+            outs[name] = fn().float()
+            res[name] = timeit(fn)
+        ref = outs["legacy"]
+        err = max(float((o - ref).abs().max()) for o in outs.values())
+        by = int(cl.sum()) * hkv * 128 * 2 * (1 if fp8 else 2)
+        rec = dict(batch=B, ctx=ctx, fp8=fp8, nsplit=ns, **{f"{n}_us": round(t, 1) for n, t in res.items()},
+                   **{f"{n}_TBps": round(by / t / 1e6, 2) for n, t in res.items()}, max_diff_vs_legacy=err)
+        out.append(rec)
+        print(json.dumps(rec), flush=True)
+    C.set_knob("decode_attn_legacy", 0)
+    C.set_knob("decode_pf", 0)
+    if a.out:
+        with open(a.out, "w") as fh:
+            json.dump(out, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()

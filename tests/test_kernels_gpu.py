@@ -158,6 +158,28 @@ def test_paged_attention_decode(hq, hkv, nsplit):
     _close(out, exp, 2e-2, 2e-2)
 
 
+@pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8)])
+def test_paged_attention_decode_one_wave_kernel(hq, hkv):
+    """>= 2048 (seq, kv head) items select the one-wave-per-item decode kernel: ragged contexts from 1 token to past
+    the 64-entry block-table window (1100 tokens = 69 blocks), prefetch on and off, against the fp32 reference."""
+    from chronos import ops
+    from chronos.ops import reference as ref
+
+    g = torch.Generator().manual_seed(hq)
+    ctx_lens = torch.randint(1, 260, (260,), generator=g).tolist()
+    ctx_lens[:6] = [1, 16, 17, 1024, 1025, 1100]
+    q, k, v, bt, qs, ctx = _attn_case([1] * len(ctx_lens), ctx_lens, hq, hkv, 16, seed=hq + 1)
+    exp = ref.paged_attention(q, k, v, bt, qs, ctx, None, len(ctx_lens), 1, 1)
+    C = torch.ops.chronos
+    try:
+        for pf in (0, 1):
+            C.set_knob("decode_pf", pf)
+            out = ops.paged_attention(q, k, v, bt, qs, ctx, None, len(ctx_lens), 1, 1)
+            _close(out, exp, 2e-2, 2e-2)
+    finally:
+        C.set_knob("decode_pf", 0)
+
+
 def test_paged_attention_spike_rescale():
     """Force the online-softmax rescale: one key dominates late in a long context."""
     from chronos import ops
@@ -293,6 +315,25 @@ def test_gemv_fused_swiglu(m):
     assert ops.gate_up_silu(x, w).shape == (m, 1792)
 
 
+@pytest.mark.parametrize("m,n,k,stages", [(3, 256, 128, 3), (100, 384, 640, 2), (129, 1024, 4096, 3),
+                                          (300, 512, 1024, 4), (1024, 4096, 256, 3)])
+@pytest.mark.parametrize("swiglu", [False, True])
+def test_mfma_gemm_matches_fp32(m, n, k, stages, swiglu):
+    """csrc/kernels/gemm.hip vs an fp32 reference: ragged M (clamped loads, masked stores), multi-stage LDS-DMA ring
+    incl. K shorter than the ring, asymmetric data (catches a transposed fragment map), fused SwiGLU epilogue."""
+    from chronos.ops import gemm
+    from chronos.ops import reference as ref
+
+    g = torch.Generator(device=DEV).manual_seed(m + n + k)
+    x = (torch.randn(m, k, device=DEV, generator=g) + torch.arange(k, device=DEV) / k).to(torch.bfloat16)
+    w = (torch.randn(n, k, device=DEV, generator=g) * 0.05 + torch.linspace(-0.02, 0.03, n, device=DEV)[:, None])
+    w = w.to(torch.bfloat16)
+    y = gemm.mfma_gemm(x, w, swiglu, stages)
+    full = x.float() @ w.float().t()
+    exp = ref.silu_mul(full.to(torch.bfloat16)) if swiglu else full
+    _close(y, exp, 2e-2, 3e-2)
+
+
 # ---------------------------------------------------------------------------------------------------------------
 # fp8-e4m3 (OCP) KV cache
 # ---------------------------------------------------------------------------------------------------------------
@@ -340,6 +381,21 @@ def test_fp8_paged_attention(nqt):
         tt, nt = torch.tensor(tiles, dtype=torch.int32, device=DEV).view(-1, 2), len(tiles)
     out = ops.paged_attention(q, k8, v8, bt, qs, ctx, tt, nt, nqt, 2 if nqt == 1 else 1, None, 0.25, 0.5)
     exp = ref.paged_attention(q, k8, v8, bt, qs, ctx, tt, nt, nqt, 1, None, 0.25, 0.5)
+    _close(out, exp, 2e-2, 2e-2)
+
+
+def test_fp8_decode_one_wave_kernel():
+    """fp8 KV through the one-wave-per-(seq, kv head) decode kernel (>= 2048 items, no kv split)."""
+    from chronos import ops
+    from chronos.ops import reference as ref
+
+    g = torch.Generator().manual_seed(3)
+    ctx_lens = torch.randint(1, 300, (256,), generator=g).tolist()
+    ctx_lens[:3] = [1, 33, 1100]
+    q, k, v, bt, qs, ctx = _attn_case([1] * len(ctx_lens), ctx_lens, 32, 8, 16, seed=21)
+    k8, v8 = ref.to_fp8_bytes(k, 1 / 0.25), ref.to_fp8_bytes(v, 1 / 0.5)
+    out = ops.paged_attention(q, k8, v8, bt, qs, ctx, None, len(ctx_lens), 1, 1, None, 0.25, 0.5)
+    exp = ref.paged_attention(q, k8, v8, bt, qs, ctx, None, len(ctx_lens), 1, 1, None, 0.25, 0.5)
     _close(out, exp, 2e-2, 2e-2)
 
 
