@@ -9,6 +9,11 @@ independent Brain engine — the DP-replica deployment of SURVEY.md §2.5 — on
          (<= --num-predict tokens, the reference's ~60-token replies) for every chain, detokenizes and the verdict
          is parsed with json.loads, exactly as the sensor does (chronos_sensor.py:120).
 
+``--mode closed`` (opt-in) measures the same metric in steady state instead of waves: every one of the ``--streams``
+sensor streams keeps exactly one chain in flight and submits its next chain the moment its verdict returns, so a
+step is ``--streams`` completed chains with no wave boundary (no straggler tail, the prefix cache stays warm as in a
+long-running server).  The default remains the wave form above.
+
 Weights are random-init Llama-3-8B (real architecture, bf16, no checkpoint offline); data is synthetic telemetry.
 Work per GPU is fixed as N grows (weak scaling).  Rank 0 prints ONE JSON line.
 """
@@ -41,8 +46,50 @@ def parse():
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-prefix-cache", action="store_true")
     ap.add_argument("--async-harvest", action="store_true")
+    ap.add_argument("--mode", choices=["wave", "closed"], default="wave")
     ap.add_argument("--device", default="cuda")
     return ap.parse_args()
+
+
+def run_closed(a, eng, prompts, barrier, progress):
+    """Steady state: each stream resubmits on completion.  Returns (elapsed, timed requests, prefix-hit tokens)."""
+    from chronos.sensor.prompt import VERDICT_SCHEMA
+
+    done, nxt, stop = [], [0], [False]
+    # each stream's chains come from its own slice, so no prompt is ever submitted twice
+    per = len(prompts) // a.streams
+    pos = [0] * a.streams
+
+    def submit(stream):
+        if pos[stream] >= per:  # this stream ran out of fresh chains: it goes idle (never a repeat)
+            return
+        p = prompts[stream * per + pos[stream]]
+        pos[stream] += 1
+        eng.submit(p, fmt=VERDICT_SCHEMA, num_predict=a.num_predict, meta={"stream": stream}, callback=on_done)
+
+    def on_done(req):
+        done.append(req)
+        if not stop[0]:
+            submit(req.meta["stream"])
+
+    for s in range(a.streams):
+        submit(s)
+    while len(done) < a.warmup * a.streams and eng.has_work():
+        eng.step()
+    progress(f"closed-loop warmup: {len(done)} chains {dict(eng.stats)}")
+    barrier()
+    n0, hit0 = len(done), eng.stats["prefix_hit_tokens"]
+    t0 = time.perf_counter()
+    target = n0 + a.steps * a.streams
+    while len(done) < target and eng.has_work():
+        eng.step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    hits = eng.stats["prefix_hit_tokens"] - hit0
+    stop[0] = True
+    eng.run_until_idle()  # drain the in-flight chains (untimed) before the single-stream runs
+    assert len(done) >= target, "closed loop ran out of chains: generate more prompts per stream"
+    return elapsed, done[n0:target], hits
 
 
 def main():
@@ -66,7 +113,8 @@ def main():
                        prefix_cache=not a.no_prefix_cache, async_harvest=a.async_harvest, seed=0)
     eng = Engine(cfg)
     total_steps = a.warmup + a.steps
-    chains = synthetic_chains(a.streams * total_steps + a.single_stream, seed=1000 + rank)
+    per_stream = total_steps if a.mode == "wave" else 2 * total_steps + 2  # closed loop: fast streams cycle more
+    chains = synthetic_chains(a.streams * per_stream + a.single_stream, seed=1000 + rank)
     prompts = [build_prompt(c.history) for c in chains]
 
     def run_step(batch):
@@ -88,20 +136,23 @@ def main():
             print(f"[bench] {time.strftime('%H:%M:%S')} {msg}", file=sys.stderr, flush=True)
 
     progress(f"engine ready: kv blocks {eng.blocks.num_blocks}, load {eng.load_seconds:.1f}s")
-    for s in range(a.warmup):
-        t = time.perf_counter()
-        run_step(prompts[s * a.streams:(s + 1) * a.streams])
-        progress(f"warmup step {s}: {time.perf_counter() - t:.2f}s {dict(eng.stats)}")
-    barrier()
-    hit0 = eng.stats["prefix_hit_tokens"]
-    t0 = time.perf_counter()
-    timed = []
-    for s in range(a.warmup, total_steps):
-        timed += run_step(prompts[s * a.streams:(s + 1) * a.streams])
-        progress(f"step {s} done")
-    barrier()
-    elapsed = time.perf_counter() - t0
-    hits = eng.stats["prefix_hit_tokens"] - hit0
+    if a.mode == "closed":
+        elapsed, timed, hits = run_closed(a, eng, prompts[:a.streams * per_stream], barrier, progress)
+    else:
+        for s in range(a.warmup):
+            t = time.perf_counter()
+            run_step(prompts[s * a.streams:(s + 1) * a.streams])
+            progress(f"warmup step {s}: {time.perf_counter() - t:.2f}s {dict(eng.stats)}")
+        barrier()
+        hit0 = eng.stats["prefix_hit_tokens"]
+        t0 = time.perf_counter()
+        timed = []
+        for s in range(a.warmup, total_steps):
+            timed += run_step(prompts[s * a.streams:(s + 1) * a.streams])
+            progress(f"step {s} done")
+        barrier()
+        elapsed = time.perf_counter() - t0
+        hits = eng.stats["prefix_hit_tokens"] - hit0
 
     ok = 0
     for r in timed:
@@ -116,7 +167,7 @@ def main():
 
     # single-stream latency (the reference's regime: one chain in flight)
     single = []
-    for p in prompts[a.streams * total_steps:]:
+    for p in prompts[a.streams * per_stream:]:
         single += run_step([p])
     single_lat = [r.latency for r in single[1:]] or [r.latency for r in single]
 
@@ -152,6 +203,8 @@ def main():
                 "parallelism": f"dp{world}" if world > 1 else "tp1",
                 "streams_per_gpu": a.streams, "num_predict": a.num_predict,
                 "format": "verdict JSON schema (constrained decode)",
+                "mode": "wave: a step = one wave of --streams chains arriving together" if a.mode == "wave" else
+                        "closed: --streams streams each keep one chain in flight; a step = --streams completions",
             },
             "p50_verdict_latency_ms": round(1000 * statistics.median(lats), 2),
             "p99_verdict_latency_ms": round(1000 * sorted(lats)[max(0, math.ceil(0.99 * len(lats)) - 1)], 2),

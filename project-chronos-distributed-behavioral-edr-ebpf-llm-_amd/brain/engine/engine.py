@@ -193,7 +193,8 @@ class Engine:
         self._graphs: dict[int, torch.cuda.CUDAGraph] = {}
         self._graph_pool = None
         self.stats = collections.Counter()
-        self._lock = threading.Lock()
+        # re-entrant: request callbacks run on the scheduler thread and may submit follow-up requests (closed loop)
+        self._lock = threading.RLock()
         self._cancels: list[tuple[Request, str]] = []
         # ---- harvest snapshots: two pinned host copies of (state, nout, out), alternated per burst ----
         pin = self.device.type == "cuda"

@@ -180,3 +180,18 @@ def test_dp_router_two_replicas():
             assert set(json.loads(o.text)) == {"risk_score", "verdict", "reason"}
     finally:
         router.close()
+
+
+def test_closed_loop_loadgen_against_fake_brain(fake):
+    """scripts/loadgen.py (N8): closed-loop streams against the REST contract; ERROR verdicts are not counted."""
+    import importlib.util
+    import os
+
+    spec = importlib.util.spec_from_file_location(
+        "loadgen", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "scripts", "loadgen.py"))
+    lg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(lg)
+    rec = asyncio.run(lg.run_level(f"{fake.url}/api/generate", 8, 1.0, 0.2, True, 32, 0))
+    assert rec["chains"] > 8 and rec["errors"] == 0 and rec["p50_latency_ms"] > 0
+    bad = asyncio.run(lg.run_level("http://127.0.0.1:9/api/generate", 2, 0.5, 0.0, True, 32, 0))
+    assert bad["chains"] == 0 and bad["errors"] > 0
