@@ -15,6 +15,8 @@
 #include <mutex>
 #include <string>
 #include <unordered_map>
+#include <vector>
+#include <cstring>
 
 namespace chronos {
 void launch_embedding(const int32_t*, const uint16_t*, uint16_t*, int, int, int64_t, int64_t, hipStream_t);
@@ -31,6 +33,13 @@ void launch_constrained_sample(const void*, bool, int64_t, const int32_t*, int, 
                                int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, int, hipStream_t);
 void launch_gemv(const uint16_t*, int, int, const uint16_t*, int, uint16_t*, bool, hipStream_t);
 void launch_gemm(const uint16_t*, const uint16_t*, uint16_t*, int, int, int, bool, int, hipStream_t);
+void* ar_create(int, int, int64_t);
+std::vector<uint8_t> ar_handles(void*);
+void ar_open(void*, const std::vector<std::vector<uint8_t>>&);
+void ar_run(void*, const uint16_t*, uint16_t*, int64_t, int64_t, hipStream_t);
+uint32_t ar_error(void*);
+int64_t ar_capacity(void*);
+void ar_destroy(void*);
 void launch_attn_prefill(const uint16_t*, const void*, const void*, const int32_t*, int, const int32_t*,
                          const int32_t*, const int32_t*, int, uint16_t*, int, int, int, float, bool, float, float,
                          hipStream_t);
@@ -303,6 +312,39 @@ void set_knob(const std::string& name, int64_t value) {
     chronos::g_knobs[name] = (int)value;
 }
 
+// ---- K14 IPC one-shot all-reduce (allreduce.hip); the handle is the C++ object's address as an int
+int64_t ar_create(int64_t rank, int64_t world, int64_t max_bytes) {
+    return reinterpret_cast<int64_t>(chronos::ar_create((int)rank, (int)world, max_bytes));
+}
+Tensor ar_handles(int64_t h) {
+    auto v = chronos::ar_handles(reinterpret_cast<void*>(h));
+    auto t = at::empty({(int64_t)v.size()}, at::TensorOptions().dtype(at::kByte));
+    memcpy(t.data_ptr(), v.data(), v.size());
+    return t;
+}
+void ar_open(int64_t h, const Tensor& all) {
+    CHK(!all.is_cuda() && all.scalar_type() == at::kByte && all.dim() == 2, "ar_open: uint8 [world, bytes] CPU");
+    auto c = all.contiguous();
+    std::vector<std::vector<uint8_t>> v;
+    for (int64_t i = 0; i < c.size(0); ++i) {
+        const uint8_t* p = c.data_ptr<uint8_t>() + i * c.size(1);
+        v.emplace_back(p, p + c.size(1));
+    }
+    chronos::ar_open(reinterpret_cast<void*>(h), v);
+}
+void ar_all_reduce(int64_t h, const Tensor& inp, const Tensor& out, int64_t spin_limit) {
+    chk_bf16(inp, "inp");
+    chk_bf16(out, "out");
+    CHK(inp.numel() == out.numel(), "ar_all_reduce: size mismatch");
+    CHK(inp.numel() % 8 == 0 && inp.numel() <= chronos::ar_capacity(reinterpret_cast<void*>(h)),
+        "ar_all_reduce: numel must be % 8 and fit the IPC buffer");
+    c10::hip::HIPGuardMasqueradingAsCUDA g(inp.device());
+    chronos::ar_run(reinterpret_cast<void*>(h), bf(inp), bfm(out), inp.numel(), spin_limit, cur_stream());
+}
+int64_t ar_error(int64_t h) { return chronos::ar_error(reinterpret_cast<void*>(h)); }
+int64_t ar_capacity(int64_t h) { return chronos::ar_capacity(reinterpret_cast<void*>(h)); }
+void ar_destroy(int64_t h) { chronos::ar_destroy(reinterpret_cast<void*>(h)); }
+
 }  // namespace
 
 TORCH_LIBRARY(chronos, m) {
@@ -316,6 +358,13 @@ TORCH_LIBRARY(chronos, m) {
     m.def("gemv(Tensor x, Tensor w, bool swiglu) -> Tensor");
     m.def("gemm(Tensor x, Tensor w, bool swiglu, int stages=3) -> Tensor");
     m.def("set_knob(str name, int value) -> ()", &set_knob);
+    m.def("ar_create(int rank, int world, int max_bytes) -> int", &ar_create);
+    m.def("ar_handles(int h) -> Tensor", &ar_handles);
+    m.def("ar_open(int h, Tensor all) -> ()", &ar_open);
+    m.def("ar_all_reduce(int h, Tensor inp, Tensor(a!) out, int spin_limit) -> ()");
+    m.def("ar_error(int h) -> int", &ar_error);
+    m.def("ar_capacity(int h) -> int", &ar_capacity);
+    m.def("ar_destroy(int h) -> ()", &ar_destroy);
     m.def("paged_attention(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_table, Tensor q_start, "
           "Tensor ctx_len, Tensor? tiles, int ntiles, int nqt, int nsplit, float scale, float k_scale=1.0, "
           "float v_scale=1.0) -> Tensor");
@@ -334,4 +383,5 @@ TORCH_LIBRARY_IMPL(chronos, CUDA, m) {
     m.impl("gemm", &gemm);
     m.impl("paged_attention", &paged_attention);
     m.impl("constrained_sample", &constrained_sample);
+    m.impl("ar_all_reduce", &ar_all_reduce);
 }

@@ -1,0 +1,60 @@
+"""IPC one-shot all-reduce for tensor-parallel decode (kernel: csrc/kernels/allreduce.hip).
+
+Every TP rank owns a bf16 exchange buffer (two parity halves) plus an uncached flag array; the IPC handles are
+swapped once over the (gloo or RCCL) process group and every rank maps all peers' buffers.  ``all_reduce(x)`` is one
+kernel launch: publish my shard, flag every peer, wait for every peer's flag, read the W shards over xGMI and sum —
+one hop instead of a ring's 2(W-1), which is what decode-sized messages (16 KiB x tokens) are bound by.  The launch
+takes no host-side state (the epoch lives on the device), so it is captured inside the decode hipGraph like any
+other kernel.  Larger messages (prefill chunks) stay on RCCL (``TPContext.all_reduce`` picks by size).
+
+A peer that never arrives makes the kernel give up after a bounded spin and set an error word (checked by
+:meth:`check`), rather than hanging the GPU.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+class IpcAllReduce:
+    def __init__(self, group=None, max_bytes: int = 8 << 20, device: torch.device | None = None,
+                 spin_limit: int = 20_000_000):
+        from .. import ops
+
+        ops.load()
+        self.C = torch.ops.chronos
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        self.max_bytes = max_bytes
+        self.spin_limit = spin_limit
+        with torch.cuda.device(self.device):
+            self.h = self.C.ar_create(self.rank, self.world, max_bytes)
+        mine = self.C.ar_handles(self.h)
+        allh = [None] * self.world
+        dist.all_gather_object(allh, mine.numpy().tobytes(), group=group)
+        table = torch.tensor([list(b) for b in allh], dtype=torch.uint8)
+        with torch.cuda.device(self.device):
+            self.C.ar_open(self.h, table)
+        self.capacity = self.C.ar_capacity(self.h)  # elements per parity half
+
+    def fits(self, x: torch.Tensor) -> bool:
+        return x.dtype == torch.bfloat16 and x.is_cuda and x.numel() % 8 == 0 and x.numel() <= self.capacity
+
+    def all_reduce(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
+        """Sum of ``x`` over the group (a new tensor unless ``out`` is given; may alias ``x``)."""
+        x = x.contiguous()
+        out = torch.empty_like(x) if out is None else out
+        self.C.ar_all_reduce(self.h, x, out, self.spin_limit)
+        return out
+
+    def check(self) -> None:
+        if self.C.ar_error(self.h):
+            raise RuntimeError("IPC all-reduce: a peer did not arrive within the spin limit (rank desync?)")
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            torch.cuda.synchronize(self.device)
+            self.C.ar_destroy(self.h)
+            self.h = None

@@ -41,6 +41,22 @@ class TPContext:
         dist.all_reduce(x, group=self.group)
         return x
 
+    def enable_ipc_allreduce(self, max_bytes: int = 8 << 20, threshold: int = 4 << 20):
+        """Route bf16 all-reduces of at most ``threshold`` bytes to the IPC one-shot kernel (K14); larger messages
+        (prefill chunks), where a ring's link bandwidth wins over one-shot's W-fold reads, stay on RCCL."""
+        from .custom_ar import IpcAllReduce
+
+        ar = IpcAllReduce(self.group, max_bytes)
+
+        def fast(x: torch.Tensor) -> Optional[torch.Tensor]:
+            if x.numel() * x.element_size() <= threshold and ar.fits(x) and x.is_contiguous():
+                return ar.all_reduce(x, out=x)
+            return None
+
+        self.fast_allreduce = fast
+        self.ipc_allreduce = ar
+        return ar
+
     def all_gather_last(self, x: torch.Tensor) -> torch.Tensor:
         """[.., n] shards -> [.., n * world] (vocab-parallel logits)."""
         if self.world == 1:

@@ -137,10 +137,22 @@ class TPEngine:
                 return
 
 
-def init_tp(backend: str = "nccl") -> tuple[TPContext, Any]:
-    """Initialise the default process group (env:// rendezvous) + a gloo control group over the same ranks."""
+def init_tp(backend: str = "nccl", ipc_allreduce: bool | None = None) -> tuple[TPContext, Any]:
+    """Initialise the default process group (env:// rendezvous) + a gloo control group over the same ranks.  On GPUs
+    the decode all-reduces go to the IPC one-shot kernel (K14) unless ``ipc_allreduce=False`` /
+    CHRONOS_IPC_ALLREDUCE=0; if the IPC mapping cannot be set up the reason is logged and RCCL carries everything."""
+    import logging
+    import os
+
     if not dist.is_initialized():
         dist.init_process_group(backend)
     tp = TPContext.from_group()
     ctrl = dist.new_group(backend="gloo") if backend != "gloo" else None
+    if ipc_allreduce is None:
+        ipc_allreduce = backend == "nccl" and os.environ.get("CHRONOS_IPC_ALLREDUCE", "1") != "0"
+    if ipc_allreduce and tp.world > 1:
+        try:
+            tp.enable_ipc_allreduce()
+        except Exception as e:  # noqa: BLE001 — reported, and RCCL remains a complete implementation
+            logging.getLogger("chronos.tp").warning("IPC all-reduce unavailable (%s); using RCCL only", e)
     return tp, ctrl
