@@ -18,7 +18,8 @@ run() {  # name timeout cmd...
 rm -f gpurun_out/summary.log
 for s in $STEPS; do
   case $s in
-    pytest) run pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider; rc=$?
+    pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 120 \
+              --timeout-method thread; rc=$?
             if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi ;;
     smoke) run smoke 600 python -c "import __graft_entry__ as g; g.smoke()" || exit $? ;;
     kernels) run kernels 600 python scripts/bench_kernels.py --out gpurun_out/kernels.json || exit $? ;;
