@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--no-prefix-cache", action="store_true")
     ap.add_argument("--async-harvest", action="store_true")
     ap.add_argument("--mode", choices=["wave", "closed"], default="wave")
+    ap.add_argument("--weights", choices=["bf16", "fp8"], default="bf16",
+                    help="fp8 = W8A8 e4m3 projections on the block-scaled MFMA / hipBLASLt fp8 (not the headline)")
     ap.add_argument("--device", default="cuda")
     return ap.parse_args()
 
@@ -110,7 +112,8 @@ def main():
 
     cfg = EngineConfig(model=a.model, device=str(device), max_slots=a.streams, max_model_len=512,
                        default_num_predict=a.num_predict, decode_burst=a.burst, use_graphs=not a.no_graphs,
-                       prefix_cache=not a.no_prefix_cache, async_harvest=a.async_harvest, seed=0)
+                       prefix_cache=not a.no_prefix_cache, async_harvest=a.async_harvest, seed=0,
+                       weight_dtype=a.weights)
     eng = Engine(cfg)
     total_steps = a.warmup + a.steps
     per_stream = total_steps if a.mode == "wave" else 2 * total_steps + 2  # closed loop: fast streams cycle more
@@ -196,7 +199,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            "dtype": "bf16" if a.weights == "bf16" else "fp8-e4m3 W8A8 projections (bf16 norms/attention/KV/LM head)",
             "data": "synthetic syscall-chain telemetry (reference prompt template), random-init weights",
             "config": {
                 "model": a.model, "global_batch": a.streams * world, "seq_len": 512,

@@ -13,6 +13,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <mutex>
+#include <tuple>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -43,6 +44,10 @@ void ar_destroy(void*);
 void launch_attn_prefill(const uint16_t*, const void*, const void*, const int32_t*, int, const int32_t*,
                          const int32_t*, const int32_t*, int, uint16_t*, int, int, int, float, bool, float, float,
                          hipStream_t);
+void launch_quant_rows(const uint16_t*, uint16_t*, const uint16_t*, uint8_t*, float*, int, int, float, int,
+                       hipStream_t);
+void launch_qlinear(const uint8_t*, const float*, const uint8_t*, const float*, uint16_t*, int, int, int, bool,
+                    hipStream_t);
 }  // namespace chronos
 
 namespace chronos {
@@ -307,6 +312,57 @@ Tensor gemm(const Tensor& x, const Tensor& w, bool swiglu, int64_t stages) {
     return y;
 }
 
+// ---- W8A8 fp8-e4m3 path (fp8.hip).  Quantised tensors travel as uint8 (OCP e4m3fn bytes) + fp32 scales.
+// mode 0: quant(x); 1: quant(rmsnorm(x) * w); 2: resid <- bf16(x + resid), quant(rmsnorm(resid) * w);
+// 3: x = [gate | up] rows of 2F, quant(silu(gate) * up)
+std::tuple<Tensor, Tensor> quant_rows(const Tensor& x, const c10::optional<Tensor>& resid,
+                                      const c10::optional<Tensor>& w, double eps, int64_t mode) {
+    chk_bf16(x, "x");
+    CHK(mode >= 0 && mode <= 3, "quant_rows: mode in {0, 1, 2, 3}");
+    const int64_t d = mode == 3 ? x.size(-1) / 2 : x.size(-1), rows = x.numel() / x.size(-1);
+    CHK(d % 8 == 0 && d <= 16384, "quant_rows: d must be % 8 and <= 16384");
+    CHK(mode != 3 || x.size(-1) == 2 * d, "quant_rows: mode 3 needs [rows, 2F]");
+    const bool norm = mode == 1 || mode == 2;
+    if (norm) {
+        CHK(w.has_value(), "quant_rows: rmsnorm modes need w");
+        chk_bf16(*w, "w");
+        CHK(w->numel() == d, "quant_rows: w must have d entries");
+    }
+    if (mode == 2) {
+        CHK(resid.has_value(), "quant_rows: mode 2 needs resid");
+        chk_bf16(*resid, "resid");
+        CHK(resid->sizes() == x.sizes(), "quant_rows: resid shape mismatch");
+    }
+    c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+    auto q = at::empty({rows, d}, x.options().dtype(at::kByte));
+    auto s = at::empty({rows}, x.options().dtype(at::kFloat));
+    chronos::launch_quant_rows(bf(x), mode == 2 ? bfm(*resid) : nullptr, norm ? bf(*w) : nullptr,
+                               q.data_ptr<uint8_t>(), s.data_ptr<float>(), (int)rows, (int)d, (float)eps, (int)mode,
+                               cur_stream());
+    return {q, s};
+}
+
+// y = (xq @ wq.T) * xs[:, None] * ws[None, :] (bf16); swiglu: wq = [gate; up] -> silu(gate) * up
+Tensor qlinear(const Tensor& xq, const Tensor& xs, const Tensor& wq, const Tensor& ws, bool swiglu) {
+    chk_gpu(xq, "xq");
+    chk_gpu(wq, "wq");
+    chk_gpu(xs, "xs");
+    chk_gpu(ws, "ws");
+    CHK(xq.scalar_type() == at::kByte && wq.scalar_type() == at::kByte, "qlinear: xq / wq must be uint8 (e4m3fn)");
+    CHK(xs.scalar_type() == at::kFloat && ws.scalar_type() == at::kFloat, "qlinear: scales must be f32");
+    const int64_t K = xq.size(-1), M = xq.numel() / K, N = wq.size(0);
+    CHK(wq.dim() == 2 && wq.size(1) == K, "qlinear: wq must be [N, K]");
+    CHK(xs.numel() == M && ws.numel() == N, "qlinear: one scale per token row / weight row");
+    CHK(K % 128 == 0, "qlinear: K % 128 == 0");
+    CHK(N % 128 == 0 && (!swiglu || (N / 2) % 64 == 0), "qlinear: N % 128 == 0 (SwiGLU: F % 64 == 0)");
+    CHK(M < (1LL << 31) / 128 && N * K < (1LL << 40), "qlinear: size");
+    c10::hip::HIPGuardMasqueradingAsCUDA g(xq.device());
+    auto y = at::empty({M, swiglu ? N / 2 : N}, xq.options().dtype(at::kBFloat16));
+    chronos::launch_qlinear(xq.data_ptr<uint8_t>(), xs.data_ptr<float>(), wq.data_ptr<uint8_t>(), ws.data_ptr<float>(),
+                            bfm(y), (int)M, (int)N, (int)K, swiglu, cur_stream());
+    return y;
+}
+
 void set_knob(const std::string& name, int64_t value) {
     std::lock_guard<std::mutex> lk(chronos::g_knob_mu);
     chronos::g_knobs[name] = (int)value;
@@ -357,6 +413,8 @@ TORCH_LIBRARY(chronos, m) {
     m.def("silu_mul(Tensor gate_up) -> Tensor");
     m.def("gemv(Tensor x, Tensor w, bool swiglu) -> Tensor");
     m.def("gemm(Tensor x, Tensor w, bool swiglu, int stages=3) -> Tensor");
+    m.def("quant_rows(Tensor x, Tensor(a!)? resid, Tensor? w, float eps, int mode) -> (Tensor, Tensor)");
+    m.def("qlinear(Tensor xq, Tensor xs, Tensor wq, Tensor ws, bool swiglu) -> Tensor");
     m.def("set_knob(str name, int value) -> ()", &set_knob);
     m.def("ar_create(int rank, int world, int max_bytes) -> int", &ar_create);
     m.def("ar_handles(int h) -> Tensor", &ar_handles);
@@ -381,6 +439,8 @@ TORCH_LIBRARY_IMPL(chronos, CUDA, m) {
     m.impl("silu_mul", &silu_mul);
     m.impl("gemv", &gemv);
     m.impl("gemm", &gemm);
+    m.impl("quant_rows", &quant_rows);
+    m.impl("qlinear", &qlinear);
     m.impl("paged_attention", &paged_attention);
     m.impl("constrained_sample", &constrained_sample);
     m.impl("ar_all_reduce", &ar_all_reduce);

@@ -65,6 +65,7 @@ class EngineConfig:
     max_string: int = 160          # default maxLength for schema strings without one (keeps verdicts short)
     prefix_cache: bool = True      # reuse KV blocks of identical prompt prefixes (the shared CHRONOS template head)
     kv_dtype: str = "bf16"         # "bf16" or "fp8" (OCP e4m3fn, per-layer scale: half the KV bytes, 2x tokens/GPU)
+    weight_dtype: str = "bf16"     # "bf16" or "fp8": W8A8 e4m3 projections on the block-scaled MFMA (csrc/kernels/fp8.hip)
     kv_scale: float = 1.0          # fp8 KV scale (stored = value / scale)
     prefill_nqt: int = 8           # 8 = flash prefill kernel (128 query rows / workgroup); 1-2 = split-K kernel
     async_harvest: bool = False    # harvest burst k while burst k+1 runs (hides host work, delays compaction)
@@ -140,7 +141,7 @@ class Engine:
         self.tok = tokenizer or load_tokenizer(cfg.tokenizer)
         t0 = time.perf_counter()
         self.model = model or build_model(cfg.model, self.device, self.tp, cfg.seed, cfg.checkpoint,
-                                          max_position=cfg.max_model_len + 16)
+                                          max_position=cfg.max_model_len + 16, weight_dtype=cfg.weight_dtype)
         self.load_seconds = time.perf_counter() - t0
         mc = self.model.cfg
         self.bank = GrammarBank(self.tok.token_bytes_list(), self.tok.stop_ids, mc.vocab_size, cfg.grammar_capacity,

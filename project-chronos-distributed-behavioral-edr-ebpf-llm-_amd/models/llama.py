@@ -151,13 +151,36 @@ def rope_table(cfg: LlamaConfig, max_pos: int, device=None) -> torch.Tensor:
 
 
 @dataclass
+class QTensor:
+    """fp8-e4m3 (OCP) projection weight for the W8A8 path (csrc/kernels/fp8.hip): bytes [N, K] uint8 and a
+    per-output-channel f32 scale [N], w ~= bytes * scale.  Quantised after TP sharding, so a row-parallel shard's
+    scales cover exactly the K-slice it multiplies."""
+    q: torch.Tensor
+    s: torch.Tensor
+
+    @property
+    def shape(self):
+        return self.q.shape
+
+    def numel(self) -> int:
+        return self.q.numel()
+
+    def nbytes(self) -> int:
+        return self.q.numel() + 4 * self.s.numel()
+
+
+def quantize(w: torch.Tensor) -> QTensor:
+    return QTensor(*ops.reference.quantize_weight(w))
+
+
+@dataclass
 class LayerWeights:
     attn_norm: torch.Tensor
-    wqkv: torch.Tensor
-    wo: torch.Tensor
+    wqkv: "torch.Tensor | QTensor"
+    wo: "torch.Tensor | QTensor"
     mlp_norm: torch.Tensor
-    w_gu: torch.Tensor
-    w_down: torch.Tensor
+    w_gu: "torch.Tensor | QTensor"
+    w_down: "torch.Tensor | QTensor"
 
 
 @dataclass
@@ -169,10 +192,15 @@ class LlamaWeights:
     vocab_start: int = 0
 
     def nbytes(self) -> int:
-        n = self.embed.numel() + self.norm.numel() + (0 if self.lm_head is self.embed else self.lm_head.numel())
+        n = 2 * (self.embed.numel() + self.norm.numel() + (0 if self.lm_head is self.embed else self.lm_head.numel()))
         for l in self.layers:
-            n += sum(t.numel() for t in (l.attn_norm, l.wqkv, l.wo, l.mlp_norm, l.w_gu, l.w_down))
-        return 2 * n
+            for t in (l.attn_norm, l.wqkv, l.wo, l.mlp_norm, l.w_gu, l.w_down):
+                n += t.nbytes() if isinstance(t, QTensor) else 2 * t.numel()
+        return n
+
+    @property
+    def fp8(self) -> bool:
+        return bool(self.layers) and isinstance(self.layers[0].wqkv, QTensor)
 
 
 def _shard_rows(t: torch.Tensor, rank: int, world: int) -> torch.Tensor:
@@ -191,8 +219,10 @@ def _local_heads(cfg: LlamaConfig, tp: TPContext) -> tuple[int, int]:
     return cfg.num_heads // tp.world, cfg.num_kv_heads // tp.world
 
 
-def assemble_layer(cfg: LlamaConfig, tp: TPContext, full: dict, device, dtype=torch.bfloat16) -> LayerWeights:
-    """Full (unsharded) HF-named tensors of one layer -> this rank's fused shard."""
+def assemble_layer(cfg: LlamaConfig, tp: TPContext, full: dict, device, dtype=torch.bfloat16,
+                   weight_dtype: str = "bf16") -> LayerWeights:
+    """Full (unsharded) HF-named tensors of one layer -> this rank's fused shard (projections quantised to
+    per-channel e4m3 when ``weight_dtype == "fp8"``; norms stay bf16)."""
     r, w = tp.rank, tp.world
     D = cfg.head_dim
     q = full["q"].view(cfg.num_heads, D, -1)
@@ -207,11 +237,17 @@ def assemble_layer(cfg: LlamaConfig, tp: TPContext, full: dict, device, dtype=to
     w_gu = torch.cat([_shard_rows(full["gate"], r, w), _shard_rows(full["up"], r, w)], 0)
     w_down = _shard_cols(full["down"], r, w)
     cv = lambda t: t.to(device=device, dtype=dtype).contiguous()  # noqa: E731
-    return LayerWeights(cv(full["attn_norm"]), cv(wqkv), cv(wo), cv(full["mlp_norm"]), cv(w_gu), cv(w_down))
+    if weight_dtype == "fp8":
+        pj = lambda t: quantize(cv(t))  # noqa: E731
+    elif weight_dtype == "bf16":
+        pj = cv
+    else:
+        raise ValueError(f"weight_dtype must be 'bf16' or 'fp8', got {weight_dtype!r}")
+    return LayerWeights(cv(full["attn_norm"]), pj(wqkv), pj(wo), cv(full["mlp_norm"]), pj(w_gu), pj(w_down))
 
 
 def random_weights(cfg: LlamaConfig, tp: TPContext | None = None, device="cpu", seed: int = 0,
-                   dtype=torch.bfloat16) -> LlamaWeights:
+                   dtype=torch.bfloat16, weight_dtype: str = "bf16") -> LlamaWeights:
     """Random-init weights with the real architecture (the benchmark's model; no checkpoints offline).
 
     Every rank draws the FULL tensor from the same seeded generator and keeps its shard, so a TP run is numerically
@@ -245,7 +281,7 @@ def random_weights(cfg: LlamaConfig, tp: TPContext | None = None, device="cpu", 
             o=rnd(d, cfg.num_heads * D), mlp_norm=ones(d),
             gate=rnd(f, d), up=rnd(f, d), down=rnd(d, f),
         )
-        layers.append(assemble_layer(cfg, tp, full, dev, dtype))
+        layers.append(assemble_layer(cfg, tp, full, dev, dtype, weight_dtype))
         del full
     gen.manual_seed(seed * 1000003 + 999983)
     if cfg.tie_word_embeddings:
@@ -266,7 +302,8 @@ def _meta_permute(w: torch.Tensor, n_heads: int) -> torch.Tensor:
     return w.view(n_heads, d1 // n_heads // 2, 2, d2).transpose(1, 2).reshape(d1, d2)
 
 
-def load_hf(path: str, tp: TPContext | None = None, device="cpu", dtype=torch.bfloat16) -> tuple[LlamaConfig, LlamaWeights]:
+def load_hf(path: str, tp: TPContext | None = None, device="cpu", dtype=torch.bfloat16,
+            weight_dtype: str = "bf16") -> tuple[LlamaConfig, LlamaWeights]:
     """HF layout: config.json + model*.safetensors (tensor names: SURVEY.md App. B)."""
     from safetensors import safe_open
 
@@ -300,7 +337,7 @@ def load_hf(path: str, tp: TPContext | None = None, device="cpu", dtype=torch.bf
             v=get(p + "self_attn.v_proj.weight"), o=get(p + "self_attn.o_proj.weight"),
             gate=get(p + "mlp.gate_proj.weight"), up=get(p + "mlp.up_proj.weight"), down=get(p + "mlp.down_proj.weight"),
         )
-        layers.append(assemble_layer(cfg, tp, full, device, dtype))
+        layers.append(assemble_layer(cfg, tp, full, device, dtype, weight_dtype))
     norm = get("model.norm.weight").to(device=device, dtype=dtype)
     if cfg.tie_word_embeddings or "lm_head.weight" not in index:
         lm_head = embed
@@ -309,7 +346,8 @@ def load_hf(path: str, tp: TPContext | None = None, device="cpu", dtype=torch.bf
     return cfg, LlamaWeights(embed, layers, norm, lm_head, vocab_start=tp.rank * vs)
 
 
-def load_meta(path: str, tp: TPContext | None = None, device="cpu", dtype=torch.bfloat16) -> tuple[LlamaConfig, LlamaWeights]:
+def load_meta(path: str, tp: TPContext | None = None, device="cpu", dtype=torch.bfloat16,
+              weight_dtype: str = "bf16") -> tuple[LlamaConfig, LlamaWeights]:
     """Meta layout: params.json + consolidated.NN.pth (model-parallel shards are concatenated back first).
     Loaded with ``weights_only=True`` (no pickled code is ever executed)."""
     tp = tp or TPContext.single()
@@ -337,17 +375,17 @@ def load_meta(path: str, tp: TPContext | None = None, device="cpu", dtype=torch.
             gate=cat(p + "feed_forward.w1.weight", 0), up=cat(p + "feed_forward.w3.weight", 0),
             down=cat(p + "feed_forward.w2.weight", 1),
         )
-        layers.append(assemble_layer(cfg, tp, full, device, dtype))
+        layers.append(assemble_layer(cfg, tp, full, device, dtype, weight_dtype))
     norm = cat("norm.weight", 0).to(device=device, dtype=dtype)
     lm_head = cat("output.weight", 0)[tp.rank * vs:(tp.rank + 1) * vs].to(device=device, dtype=dtype).contiguous()
     return cfg, LlamaWeights(embed, layers, norm, lm_head, vocab_start=tp.rank * vs)
 
 
-def load_checkpoint(path: str, tp: TPContext | None = None, device="cpu"):
+def load_checkpoint(path: str, tp: TPContext | None = None, device="cpu", weight_dtype: str = "bf16"):
     if os.path.exists(os.path.join(path, "config.json")):
-        return load_hf(path, tp, device)
+        return load_hf(path, tp, device, weight_dtype=weight_dtype)
     if os.path.exists(os.path.join(path, "params.json")):
-        return load_meta(path, tp, device)
+        return load_meta(path, tp, device, weight_dtype=weight_dtype)
     raise FileNotFoundError(f"{path}: neither an HF (config.json) nor a Meta (params.json) Llama checkpoint")
 
 
@@ -462,20 +500,36 @@ class LlamaModel:
         h = ops.embedding(sb.ids, w.embed, w.vocab_start)
         h = tp.all_reduce(h)
         resid = h
-        x = ops.rmsnorm(h, w.layers[0].attn_norm, eps)
+        fp8 = w.fp8
+        # W8A8 path: every projection input is produced directly as (e4m3 bytes, per-token scale) by the kernel that
+        # already holds the row — the (residual +) RMSNorm, or a quantising pass over the attention / SwiGLU output
+        if fp8:
+            xq, xs = ops.quant_rows(h, None, w.layers[0].attn_norm, eps, 1)
+        else:
+            x = ops.rmsnorm(h, w.layers[0].attn_norm, eps)
         q_buf = torch.empty(T, self.hq, cfg.head_dim, device=h.device, dtype=h.dtype)
         for li, lw in enumerate(w.layers):
-            qkv = ops.linear(x, lw.wqkv)
+            qkv = ops.qlinear(xq, xs, lw.wqkv.q, lw.wqkv.s) if fp8 else ops.linear(x, lw.wqkv)
             ops.rope_kv_write(qkv, sb.pos, sb.tok_seq, sb.block_table, self.cos_sin, q_buf, kv.k[li], kv.v[li],
                               self.hq, self.hkv, True, kv.k_scale[li], kv.v_scale[li])
             attn = ops.paged_attention(q_buf, kv.k[li], kv.v[li], sb.block_table, sb.q_start, sb.ctx_len, sb.tiles,
                                        sb.ntiles, sb.nqt, sb.nsplit, self.scale, kv.k_scale[li], kv.v_scale[li])
-            o = tp.all_reduce(ops.linear(attn.view(T, -1), lw.wo))
-            x = ops.add_rmsnorm(o, resid, lw.mlp_norm, eps)
-            a = ops.gate_up_silu(x, lw.w_gu)
-            dn = tp.all_reduce(ops.linear(a, lw.w_down))
+            if fp8:
+                aq, asc = ops.quant_rows(attn.view(T, -1))
+                o = tp.all_reduce(ops.qlinear(aq, asc, lw.wo.q, lw.wo.s))
+                xq, xs = ops.quant_rows(o, resid, lw.mlp_norm, eps, 2)
+                aq, asc = ops.qgate_up_quant(xq, xs, lw.w_gu.q, lw.w_gu.s)
+                dn = tp.all_reduce(ops.qlinear(aq, asc, lw.w_down.q, lw.w_down.s))
+            else:
+                o = tp.all_reduce(ops.linear(attn.view(T, -1), lw.wo))
+                x = ops.add_rmsnorm(o, resid, lw.mlp_norm, eps)
+                a = ops.gate_up_silu(x, lw.w_gu)
+                dn = tp.all_reduce(ops.linear(a, lw.w_down))
             if li + 1 < len(w.layers):
-                x = ops.add_rmsnorm(dn, resid, w.layers[li + 1].attn_norm, eps)
+                if fp8:
+                    xq, xs = ops.quant_rows(dn, resid, w.layers[li + 1].attn_norm, eps, 2)
+                else:
+                    x = ops.add_rmsnorm(dn, resid, w.layers[li + 1].attn_norm, eps)
             else:  # only the sampled rows need the final norm + LM head
                 dl = dn.index_select(0, sb.last_idx)
                 rl = resid.index_select(0, sb.last_idx)
@@ -486,13 +540,16 @@ class LlamaModel:
 
 
 def build_model(preset: str | LlamaConfig = "tiny", device="cpu", tp: TPContext | None = None, seed: int = 0,
-                checkpoint: str | None = None, max_position: int | None = None) -> LlamaModel:
+                checkpoint: str | None = None, max_position: int | None = None,
+                weight_dtype: str = "bf16") -> LlamaModel:
+    """``weight_dtype="fp8"``: projections as per-channel e4m3 + W8A8 fp8 MFMA GEMMs (embedding, norms, LM head, attention
+    and the KV cache keep their own dtypes)."""
     tp = tp or TPContext.single()
     if checkpoint:
-        cfg, w = load_checkpoint(checkpoint, tp, device)
+        cfg, w = load_checkpoint(checkpoint, tp, device, weight_dtype)
     else:
         cfg = preset if isinstance(preset, LlamaConfig) else get_config(preset)
-        w = random_weights(cfg, tp, device, seed)
+        w = random_weights(cfg, tp, device, seed, weight_dtype=weight_dtype)
     return LlamaModel(cfg, w, tp, device, max_position)
 
 

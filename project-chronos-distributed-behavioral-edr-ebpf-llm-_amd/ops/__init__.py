@@ -9,6 +9,7 @@ Kernel sources: csrc/kernels/{elementwise,attention,sampler}.hip (SURVEY.md §2.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -56,6 +57,55 @@ def silu_mul(gu: torch.Tensor) -> torch.Tensor:
     if gu.is_cuda:
         return _k().silu_mul(gu)
     return ref.silu_mul(gu)
+
+
+def quant_rows(x: torch.Tensor, resid: torch.Tensor | None = None, w: torch.Tensor | None = None, eps: float = 1e-5,
+               mode: int = 0) -> tuple[torch.Tensor, torch.Tensor]:
+    """Dynamic per-row e4m3 quantisation, optionally fused with (residual add +) RMSNorm (csrc/kernels/fp8.hip):
+    mode 0 = quant(x), 1 = quant(rmsnorm(x) * w), 2 = resid <- bf16(x + resid) then quant(rmsnorm(resid) * w),
+    3 = quant(silu(gate) * up) of [gate | up] rows."""
+    if x.is_cuda:
+        return _k().quant_rows(x, resid, w, eps, mode)
+    return ref.quant_rows(x, resid, w, eps, mode)
+
+
+# W8A8 GEMM routing, by measured shape (profiles/r1_fp8_gemm.json): the hand-written kernels where they win — the fp8
+# decode GEMV (M <= 4) and the MFMA GEMM with the fused SwiGLU epilogue for gate_up at M <= 128 — and hipBLASLt's fp8
+# GEMM with row-wise scales (torch._scaled_mm, a plain library GEMM) for the large tiles.  CHRONOS_QGEMM=own|lib|auto.
+_QGEMM = os.environ.get("CHRONOS_QGEMM", "auto")
+_F8 = torch.float8_e4m3fn
+
+
+def _qown(m: int, n: int, k: int, swiglu: bool) -> bool:
+    if _QGEMM != "auto":
+        return _QGEMM == "own"
+    return (m <= 4 and k % 1024 == 0) or (swiglu and m <= 128)
+
+
+def _qlib(xq, xs, wq, ws) -> torch.Tensor:
+    return torch._scaled_mm(xq.view(_F8), wq.view(_F8).t(), scale_a=xs.view(-1, 1), scale_b=ws.view(1, -1),
+                            out_dtype=torch.bfloat16)
+
+
+def qlinear(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor, swiglu: bool = False) -> torch.Tensor:
+    """W8A8 fp8 projection: y = (xq @ wq.T) * xs * ws in bf16 (swiglu: wq = [gate; up] -> silu(gate) * up)."""
+    if xq.is_cuda:
+        m, k = xq.numel() // xq.shape[-1], xq.shape[-1]
+        if _qown(m, wq.shape[0], k, swiglu):
+            return _k().qlinear(xq, xs, wq, ws, swiglu)
+        y = _qlib(xq, xs, wq, ws)
+        return silu_mul(y) if swiglu else y
+    return ref.qlinear(xq, xs, wq, ws, swiglu)
+
+
+def qgate_up_quant(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor):
+    """The MLP's fp8 middle: (e4m3 bytes, row scale) of silu(x Wg^T) * (x Wu^T), ready for the down projection.
+    Fused SwiGLU GEMM epilogue + row quant at small M; library GEMM + one fused SwiGLU-and-quantise pass otherwise."""
+    if xq.is_cuda:
+        m, k = xq.numel() // xq.shape[-1], xq.shape[-1]
+        if not _qown(m, wq.shape[0], k, True):
+            return quant_rows(_qlib(xq, xs, wq, ws), mode=3)
+    return quant_rows(qlinear(xq, xs, wq, ws, True))
 
 
 def rope_kv_write(qkv, pos, tok_seq, block_table, cos_sin, q_out, k_cache, v_cache, hq: int, hkv: int,

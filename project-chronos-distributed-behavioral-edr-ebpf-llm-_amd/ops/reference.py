@@ -46,6 +46,52 @@ def from_fp8_bytes(b: torch.Tensor, scale: float) -> torch.Tensor:
     return b.view(torch.float8_e4m3fn).float() * scale
 
 
+def quant_rows(x: torch.Tensor, resid: torch.Tensor | None = None, w: torch.Tensor | None = None, eps: float = 1e-5,
+               mode: int = 0) -> tuple[torch.Tensor, torch.Tensor]:
+    """Per-row dynamic e4m3 quantisation (fp8.hip quant_rows_kernel): mode 0 = x, 1 = rmsnorm(x) * w,
+    2 = resid <- bf16(x + resid), rmsnorm(resid) * w, 3 = silu(gate) * up of [gate | up] rows.
+    Returns (bytes [rows, d] uint8, scale [rows] f32)."""
+    d = x.shape[-1]
+    if mode == 3:
+        y = silu_mul(x)
+        d = d // 2
+    elif mode == 2:
+        y = add_rmsnorm(x, resid, w, eps)
+    elif mode == 1:
+        y = rmsnorm(x, w, eps)
+    else:
+        y = x
+    y = y.reshape(-1, d).float()
+    amax = y.abs().amax(-1)
+    s = torch.where(amax > 0, amax / FP8_MAX, torch.ones_like(amax))
+    r = torch.where(amax > 0, FP8_MAX / amax, torch.ones_like(amax))
+    q = (y * r[:, None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn).view(torch.uint8)
+    return q, s
+
+
+def qlinear(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: torch.Tensor, swiglu: bool = False) -> torch.Tensor:
+    """fp32 reference of the W8A8 GEMM: (dequant(xq) @ dequant(wq).T), bf16 out; swiglu: wq = [gate; up]."""
+    x = xq.view(torch.float8_e4m3fn).float()
+    wf = wq.view(torch.float8_e4m3fn).float()
+    acc = x @ wf.t()
+    y = acc * xs.float()[:, None] * ws.float()[None, :]
+    if not swiglu:
+        return y.to(torch.bfloat16)
+    f = y.shape[-1] // 2
+    g = y[:, :f].to(torch.bfloat16).float()
+    u = y[:, f:].to(torch.bfloat16).float()
+    return (torch.nn.functional.silu(g).to(torch.bfloat16).float() * u).to(torch.bfloat16)
+
+
+def quantize_weight(w: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+    """Per-output-channel e4m3 weight quantisation: (bytes [N, K] uint8, scale [N] f32), w ~= bytes * scale."""
+    wf = w.float()
+    amax = wf.abs().amax(-1).clamp_min(1e-12)
+    s = amax / FP8_MAX
+    q = (wf / s[:, None]).clamp(-FP8_MAX, FP8_MAX).to(torch.float8_e4m3fn).view(torch.uint8)
+    return q.contiguous(), s.contiguous()
+
+
 def rope_kv_write(qkv, pos, tok_seq, block_table, cos_sin, q_out, k_cache, v_cache, hq: int, hkv: int,
                   write_q: bool = True, k_scale: float = 1.0, v_scale: float = 1.0) -> None:
     T = qkv.shape[0]
