@@ -70,6 +70,8 @@ class EngineConfig:
     prefill_nqt: int = 8           # 8 = flash prefill kernel (128 query rows / workgroup); 1-2 = split-K kernel
     async_harvest: bool = False    # harvest burst k while burst k+1 runs (hides host work, delays compaction)
     request_timeout_s: float = 0.0  # >0: a request not finished this long after submit is cancelled (reason "timeout")
+    tp_overlap: bool = True        # TP prefill: two micro-batches, each one's RCCL all-reduces overlap the other's compute
+    tp_overlap_min_tokens: int = 1024
 
 
 @dataclass
@@ -393,8 +395,10 @@ class Engine:
             bts.append(req.blocks)
             reqs.append(req)
             budget -= n
+        ntok = sum(len(c) for c in chunks)
+        split = 2 if (self.tp.world > 1 and self.cfg.tp_overlap and ntok >= self.cfg.tp_overlap_min_tokens) else 1
         sb = make_prefill_batch(chunks, starts, bts, self.model.cfg, self.tp, self.device,
-                                max_blocks=self.max_blocks_per_seq, nqt=self.cfg.prefill_nqt)
+                                max_blocks=self.max_blocks_per_seq, nqt=self.cfg.prefill_nqt, split=split)
         logits = self.model.forward(sb, self.kv)
         done_rows, done_reqs = [], []
         for i, (req, ch) in enumerate(zip(reqs, chunks)):

@@ -433,13 +433,31 @@ class StepBatch:
     ntiles: int
     nqt: int = 1
     nsplit: int = 1
+    # micro-batches over contiguous sequence ranges (TP prefill): the forward interleaves them layer by layer so the
+    # RCCL all-reduce of one runs on its stream while the other computes (LlamaModel.forward)
+    parts: Optional[list] = None
 
 
 def make_prefill_batch(prompts: list[list[int]], starts: list[int], block_tables: list[list[int]], cfg: LlamaConfig,
                        tp: TPContext, device, max_blocks: int | None = None, nqt: int = 2,
-                       ctx_totals: list[int] | None = None) -> StepBatch:
+                       ctx_totals: list[int] | None = None, split: int = 1) -> StepBatch:
     """Host builder for a (chunked) prefill step.  prompts[b] are the tokens of this chunk, starts[b] the position of
-    its first token (prefix already in the cache)."""
+    its first token (prefix already in the cache).  ``split > 1`` also builds that many token-balanced micro-batches
+    of whole sequences (``StepBatch.parts``) for communication/compute overlap under tensor parallelism."""
+    if split > 1 and len(prompts) >= split:
+        total = sum(len(t) for t in prompts)
+        cuts, acc, b0 = [], 0, 0
+        for b, t in enumerate(prompts):
+            acc += len(t)
+            if len(cuts) < split - 1 and acc >= total * (len(cuts) + 1) / split and b + 1 < len(prompts):
+                cuts.append(b + 1)
+        bounds = [0] + cuts + [len(prompts)]
+        whole = make_prefill_batch(prompts, starts, block_tables, cfg, tp, device, max_blocks, nqt, ctx_totals)
+        whole.parts = [make_prefill_batch(prompts[a:b], starts[a:b], block_tables[a:b], cfg, tp, device, max_blocks,
+                                          nqt) for a, b in zip(bounds, bounds[1:]) if b > a]
+        if len(whole.parts) < 2:
+            whole.parts = None
+        return whole
     hq, hkv = _local_heads(cfg, tp)
     ids, pos, tok_seq, qs = [], [], [], [0]
     for b, (toks, s0) in enumerate(zip(prompts, starts)):
@@ -474,7 +492,7 @@ def h2d(t: torch.Tensor | None, device) -> torch.Tensor | None:
 def to_device(sb: StepBatch, device) -> StepBatch:
     mv = lambda t: h2d(t, device)  # noqa: E731
     return StepBatch(mv(sb.ids), mv(sb.pos), mv(sb.tok_seq), mv(sb.block_table), mv(sb.q_start), mv(sb.ctx_len),
-                     mv(sb.last_idx), mv(sb.tiles), sb.ntiles, sb.nqt, sb.nsplit)
+                     mv(sb.last_idx), mv(sb.tiles), sb.ntiles, sb.nqt, sb.nsplit, sb.parts)
 
 
 # -----------------------------------------------------------------------------------------------------------------
@@ -492,48 +510,71 @@ class LlamaModel:
         self.cos_sin = rope_table(cfg, max_position or cfg.max_position, self.device)
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
 
+    # ---- one micro-batch's pieces of a layer (bf16: x is a tensor; W8A8: x is (e4m3 bytes, row scales)) ----------
+    def _norm(self, h: torch.Tensor, resid: torch.Tensor | None, w: torch.Tensor):
+        """(resid <- h + resid) and the normalised projection input."""
+        eps = self.cfg.rms_eps
+        if self.w.fp8:
+            return ops.quant_rows(h, resid, w, eps, 1 if resid is None else 2)
+        return ops.rmsnorm(h, w, eps) if resid is None else ops.add_rmsnorm(h, resid, w, eps)
+
+    def _attn(self, li: int, lw: LayerWeights, st: dict, kv: KVCache) -> torch.Tensor:
+        """Attention block up to the row-parallel o_proj; returns this rank's partial sum."""
+        sb, T, x = st["sb"], st["T"], st["x"]
+        qkv = ops.qlinear(*x, lw.wqkv.q, lw.wqkv.s) if self.w.fp8 else ops.linear(x, lw.wqkv)
+        ops.rope_kv_write(qkv, sb.pos, sb.tok_seq, sb.block_table, self.cos_sin, st["q_buf"], kv.k[li], kv.v[li],
+                          self.hq, self.hkv, True, kv.k_scale[li], kv.v_scale[li])
+        attn = ops.paged_attention(st["q_buf"], kv.k[li], kv.v[li], sb.block_table, sb.q_start, sb.ctx_len, sb.tiles,
+                                   sb.ntiles, sb.nqt, sb.nsplit, self.scale, kv.k_scale[li], kv.v_scale[li])
+        if self.w.fp8:
+            return ops.qlinear(*ops.quant_rows(attn.view(T, -1)), lw.wo.q, lw.wo.s)
+        return ops.linear(attn.view(T, -1), lw.wo)
+
+    def _mlp(self, lw: LayerWeights, st: dict) -> torch.Tensor:
+        """SwiGLU MLP up to the row-parallel down_proj; returns this rank's partial sum."""
+        x = st["x"]
+        if self.w.fp8:
+            return ops.qlinear(*ops.qgate_up_quant(*x, lw.w_gu.q, lw.w_gu.s), lw.w_down.q, lw.w_down.s)
+        return ops.linear(ops.gate_up_silu(x, lw.w_gu), lw.w_down)
+
     def forward(self, sb: StepBatch, kv: KVCache, logits_dtype=torch.bfloat16) -> torch.Tensor:
-        """Returns logits [B, V] for the token at sb.last_idx of every sequence (full vocab on every TP rank)."""
+        """Returns logits [B, V] for the token at sb.last_idx of every sequence (full vocab on every TP rank).
+
+        With TP and ``sb.parts`` (prefill), the micro-batches run interleaved: every layer issues each part's o_proj
+        all-reduce asynchronously (RCCL runs it on its own HIP stream) and moves on to the next part's attention, then
+        waits for it before that part's MLP, whose down_proj all-reduce in turn overlaps the next part's MLP / the next
+        layer's attention — xGMI time hides behind compute instead of adding to it (SURVEY.md §5.8 overlap).
+        Single part (decode, TP=1): the same ops in the same order with synchronous all-reduces (graph-capturable, the
+        IPC one-shot kernel for decode-sized messages)."""
         cfg, w, tp = self.cfg, self.w, self.tp
-        T = sb.ids.numel()
-        eps = cfg.rms_eps
-        h = ops.embedding(sb.ids, w.embed, w.vocab_start)
-        h = tp.all_reduce(h)
-        resid = h
-        fp8 = w.fp8
-        # W8A8 path: every projection input is produced directly as (e4m3 bytes, per-token scale) by the kernel that
-        # already holds the row — the (residual +) RMSNorm, or a quantising pass over the attention / SwiGLU output
-        if fp8:
-            xq, xs = ops.quant_rows(h, None, w.layers[0].attn_norm, eps, 1)
-        else:
-            x = ops.rmsnorm(h, w.layers[0].attn_norm, eps)
-        q_buf = torch.empty(T, self.hq, cfg.head_dim, device=h.device, dtype=h.dtype)
+        parts = sb.parts if (sb.parts and tp.world > 1) else [sb]
+        overlap = len(parts) > 1
+        ar = (lambda t: tp.all_reduce_async(t)) if overlap else (lambda t: (tp.all_reduce(t), None))  # noqa: E731
+        states = []
+        for p in parts:
+            h = tp.all_reduce(ops.embedding(p.ids, w.embed, w.vocab_start))
+            T = p.ids.numel()
+            states.append(dict(sb=p, T=T, resid=h, x=self._norm(h, None, w.layers[0].attn_norm),
+                               q_buf=torch.empty(T, self.hq, cfg.head_dim, device=h.device, dtype=h.dtype)))
+        L = len(w.layers)
         for li, lw in enumerate(w.layers):
-            qkv = ops.qlinear(xq, xs, lw.wqkv.q, lw.wqkv.s) if fp8 else ops.linear(x, lw.wqkv)
-            ops.rope_kv_write(qkv, sb.pos, sb.tok_seq, sb.block_table, self.cos_sin, q_buf, kv.k[li], kv.v[li],
-                              self.hq, self.hkv, True, kv.k_scale[li], kv.v_scale[li])
-            attn = ops.paged_attention(q_buf, kv.k[li], kv.v[li], sb.block_table, sb.q_start, sb.ctx_len, sb.tiles,
-                                       sb.ntiles, sb.nqt, sb.nsplit, self.scale, kv.k_scale[li], kv.v_scale[li])
-            if fp8:
-                aq, asc = ops.quant_rows(attn.view(T, -1))
-                o = tp.all_reduce(ops.qlinear(aq, asc, lw.wo.q, lw.wo.s))
-                xq, xs = ops.quant_rows(o, resid, lw.mlp_norm, eps, 2)
-                aq, asc = ops.qgate_up_quant(xq, xs, lw.w_gu.q, lw.w_gu.s)
-                dn = tp.all_reduce(ops.qlinear(aq, asc, lw.w_down.q, lw.w_down.s))
-            else:
-                o = tp.all_reduce(ops.linear(attn.view(T, -1), lw.wo))
-                x = ops.add_rmsnorm(o, resid, lw.mlp_norm, eps)
-                a = ops.gate_up_silu(x, lw.w_gu)
-                dn = tp.all_reduce(ops.linear(a, lw.w_down))
-            if li + 1 < len(w.layers):
-                if fp8:
-                    xq, xs = ops.quant_rows(dn, resid, w.layers[li + 1].attn_norm, eps, 2)
-                else:
-                    x = ops.add_rmsnorm(dn, resid, w.layers[li + 1].attn_norm, eps)
-            else:  # only the sampled rows need the final norm + LM head
-                dl = dn.index_select(0, sb.last_idx)
-                rl = resid.index_select(0, sb.last_idx)
-                x = ops.add_rmsnorm(dl, rl, w.norm, eps)
+            pend = [ar(self._attn(li, lw, st, kv)) for st in states]
+            pend2 = []
+            for st, (o, work) in zip(states, pend):
+                if work is not None:
+                    work.wait()
+                st["x"] = self._norm(o, st["resid"], lw.mlp_norm)
+                pend2.append(ar(self._mlp(lw, st)))
+            for st, (dn, work) in zip(states, pend2):
+                if work is not None:
+                    work.wait()
+                if li + 1 < L:
+                    st["x"] = self._norm(dn, st["resid"], w.layers[li + 1].attn_norm)
+                else:  # only the sampled rows need the final norm + LM head (bf16)
+                    li_ = st["sb"].last_idx
+                    st["x"] = ops.add_rmsnorm(dn.index_select(0, li_), st["resid"].index_select(0, li_), w.norm,
+                                              cfg.rms_eps)
+        x = states[0]["x"] if len(states) == 1 else torch.cat([st["x"] for st in states])
         logits = ops.linear(x, w.lm_head)
         logits = tp.all_gather_last(logits)
         return logits if logits.dtype == logits_dtype else logits.to(logits_dtype)

@@ -41,6 +41,13 @@ class TPContext:
         dist.all_reduce(x, group=self.group)
         return x
 
+    def all_reduce_async(self, x: torch.Tensor):
+        """Start a sum all-reduce without blocking the compute stream; returns (x, work) — call ``work.wait()`` before
+        reading x (on GPU that makes the current HIP stream wait for RCCL's stream, nothing blocks on the host)."""
+        if self.world == 1:
+            return x, None
+        return x, dist.all_reduce(x, group=self.group, async_op=True)
+
     def enable_ipc_allreduce(self, max_bytes: int = 8 << 20, threshold: int = 4 << 20):
         """Route bf16 all-reduces of at most ``threshold`` bytes to the IPC one-shot kernel (K14); larger messages
         (prefill chunks), where a ring's link bandwidth wins over one-shot's W-fold reads, stay on RCCL."""

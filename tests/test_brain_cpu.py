@@ -118,10 +118,10 @@ def test_grammar_bank_walk(tok):
 # model consistency (reference ops)
 # ---------------------------------------------------------------------------------------------------------------
 
-def _logits(model, kv, prompts, starts, bts):
+def _logits(model, kv, prompts, starts, bts, split=1):
     from chronos.models.llama import make_prefill_batch
 
-    sb = make_prefill_batch(prompts, starts, bts, model.cfg, model.tp, "cpu", max_blocks=8)
+    sb = make_prefill_batch(prompts, starts, bts, model.cfg, model.tp, "cpu", max_blocks=8, split=split)
     return model.forward(sb, kv).float()
 
 
@@ -248,8 +248,12 @@ def _tp_worker(rank, world, port, q):
     m = build_model("tiny", "cpu", tp=tp, seed=4)
     kv = KVCache(m.cfg, tp, 16, 16, "cpu")
     out = _logits(m, kv, [list(range(40, 71)), list(range(90, 95))], [0, 0], [[1, 2], [3]])
+    # the overlapped form: two micro-batches, async all-reduces interleaved with the other part's compute
+    kv2 = KVCache(m.cfg, tp, 16, 16, "cpu")
+    out2 = _logits(m, kv2, [list(range(40, 71)), list(range(90, 95)), list(range(7, 30))], [0, 0, 0],
+                   [[1, 2], [3], [4, 5]], split=2)
     if rank == 0:
-        q.put(out)
+        q.put((out, out2))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -262,13 +266,18 @@ def test_tensor_parallel_matches_single():
     m = build_model("tiny", "cpu", seed=4)
     kv = KVCache(m.cfg, m.tp, 16, 16, "cpu")
     ref = _logits(m, kv, [list(range(40, 71)), list(range(90, 95))], [0, 0], [[1, 2], [3]])
+    kv2 = KVCache(m.cfg, m.tp, 16, 16, "cpu")
+    ref2 = _logits(m, kv2, [list(range(40, 71)), list(range(90, 95)), list(range(7, 30))], [0, 0, 0],
+                   [[1, 2], [3], [4, 5]])
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     ps = [ctx.Process(target=_tp_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in ps:
         p.start()
-    out = q.get(timeout=240)
+    out, out2 = q.get(timeout=240)
     for p in ps:
         p.join(timeout=60)
     assert torch.allclose(out, ref, atol=3e-2), float((out - ref).abs().max())
+    assert out2.shape == ref2.shape
+    assert torch.allclose(out2, ref2, atol=3e-2), float((out2 - ref2).abs().max())
