@@ -156,6 +156,8 @@ def main():
         barrier()
         elapsed = time.perf_counter() - t0
         hits = eng.stats["prefix_hit_tokens"] - hit0
+        progress("phase seconds (all steps incl. warmup): "
+                 + json.dumps({k: round(v, 3) for k, v in eng.phase_s.items()}))
 
     ok = 0
     for r in timed:

@@ -85,6 +85,25 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
 }  // namespace chronos
 
 namespace chronos {
+// ---- decode early-exit gate ------------------------------------------------------------------------------------
+// A captured decode burst runs k steps back to back.  For a small decode bucket (n <= kGateMax rows, the single- /
+// few-stream regime) every kernel of a step first reads the n slot states the previous step's sampler wrote and
+// returns at once when none is live (state > 0; DONE == 0, empty slot == -1), so the steps of a burst that follow
+// the last verdict's end cost a launch each instead of a full forward.  Set from Python around decode capture
+// (torch.ops.chronos.set_decode_gate); launchers read the host globals below and pass them as kernel arguments.
+constexpr int kGateMax = 8;
+extern const int32_t* g_gate_state;
+extern int g_gate_n;
+// launcher helper: the (state pointer, n) kernel-argument pair of the current gate, or (nullptr, 0)
+#define CHRONOS_GATE (g_gate_n > 0 && g_gate_n <= kGateMax ? g_gate_state : nullptr), \
+                     (g_gate_n > 0 && g_gate_n <= kGateMax ? g_gate_n : 0)
+__device__ __forceinline__ bool gate_closed(const int32_t* st, int n) {
+    if (n <= 0) return false;
+    bool live = false;
+    for (int i = 0; i < n; ++i) live |= st[i] > 0;
+    return !live;
+}
+
 // Host-side tuning knobs (defined in bindings.cpp): value set through torch.ops.chronos.set_knob(name, v), else the
 // environment variable CHRONOS_<NAME>, else `dflt`.  Used for in-process A/B of kernel variants
 // (cdna_hip_programming.md §5.4 rule 24: interleave variants in ONE process).

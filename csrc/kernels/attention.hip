@@ -32,8 +32,9 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
     const int32_t* __restrict__ block_table, int bt_stride, const int32_t* __restrict__ q_start,
     const int32_t* __restrict__ ctx_len, const int32_t* __restrict__ tiles, uint16_t* __restrict__ out,
     float* __restrict__ part_o, float* __restrict__ part_lse, int hq, int hkv, int block_size, float scale_log2,
-    float k_scale, float v_scale) {
+    float k_scale, float v_scale, const int32_t* __restrict__ gst, int gn) {
     constexpr int ROWS = NQT * 16;
+    if (gate_closed(gst, gn)) return;
     const uint16_t* kc = reinterpret_cast<const uint16_t*>(kcv);
     const uint16_t* vc = reinterpret_cast<const uint16_t*>(vcv);
     const uint8_t* kc8 = reinterpret_cast<const uint8_t*>(kcv);
@@ -242,8 +243,10 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
 template <int NQT>
 __global__ void __launch_bounds__(256) paged_attn_combine_kernel(
     const float* __restrict__ part_o, const float* __restrict__ part_lse, const int32_t* __restrict__ q_start,
-    const int32_t* __restrict__ tiles, uint16_t* __restrict__ out, int hq, int hkv, int nsplit, int ntiles) {
+    const int32_t* __restrict__ tiles, uint16_t* __restrict__ out, int hq, int hkv, int nsplit, int ntiles,
+    const int32_t* __restrict__ gst, int gn) {
     constexpr int ROWS = NQT * 16;
+    if (gate_closed(gst, gn)) return;
     const int tile = blockIdx.x, h = blockIdx.y, G = hq / hkv;
     int rel0, qbase, qlen;
     if (tiles) {
@@ -296,8 +299,10 @@ template <bool FP8, bool PF>
 __global__ void __launch_bounds__(256) paged_decode_kernel(
     const uint16_t* __restrict__ q, const void* __restrict__ kcv, const void* __restrict__ vcv,
     const int32_t* __restrict__ block_table, int bt_stride, const int32_t* __restrict__ ctx_len,
-    uint16_t* __restrict__ out, int nitems, int hq, int hkv, float scale_log2, float k_scale, float v_scale) {
-    constexpr int block_size = 16;  // the engine's page size; compile-time so every K/V address is base + immediate
+    uint16_t* __restrict__ out, int nitems, int hq, int hkv, float scale_log2, float k_scale, float v_scale,
+    const int32_t* __restrict__ gst, int gn) {
+    constexpr int block_size = 16;
+    if (gate_closed(gst, gn)) return;  // the engine's page size; compile-time so every K/V address is base + immediate
     const int lane = threadIdx.x & 63;
     const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (item >= nitems) return;  // whole wave; the kernel has no workgroup-level synchronisation
@@ -475,7 +480,7 @@ void launch_paged_attn(const uint16_t* q, const void* kc, const void* vc, const 
         const int pf = knob("decode_pf", 0);
 #define PD_LAUNCH(F, P)                                                                                         \
     hipLaunchKernelGGL((paged_decode_kernel<F, P>), dim3((nitems + 3) / 4), dim3(256), 0, st, q, kc, vc, block_table, \
-                       bt_stride, ctx_len, out, nitems, hq, hkv, scale_log2, k_scale, v_scale)
+                       bt_stride, ctx_len, out, nitems, hq, hkv, scale_log2, k_scale, v_scale, CHRONOS_GATE)
         if (fp8) {
             if (pf) PD_LAUNCH(true, true); else PD_LAUNCH(true, false);
         } else {
@@ -489,7 +494,8 @@ legacy:
     const size_t sh = paged_attn_smem(nqt);
 #define PA_LAUNCH(N, F)                                                                                         \
     hipLaunchKernelGGL((paged_attn_kernel<N, F>), grid, block, sh, st, q, kc, vc, block_table, bt_stride, q_start, \
-                       ctx_len, tiles, out, part_o, part_lse, hq, hkv, block_size, scale_log2, k_scale, v_scale)
+                       ctx_len, tiles, out, part_o, part_lse, hq, hkv, block_size, scale_log2, k_scale, v_scale, \
+                       CHRONOS_GATE)
     if (nqt == 1) {
         if (fp8) PA_LAUNCH(1, true); else PA_LAUNCH(1, false);
     } else {
@@ -507,10 +513,10 @@ legacy:
     if (nsplit > 1) {
         if (nqt == 1)
             hipLaunchKernelGGL(paged_attn_combine_kernel<1>, dim3(ntiles, hkv), block, 0, st, part_o, part_lse,
-                               q_start, tiles, out, hq, hkv, nsplit, ntiles);
+                               q_start, tiles, out, hq, hkv, nsplit, ntiles, CHRONOS_GATE);
         else
             hipLaunchKernelGGL(paged_attn_combine_kernel<2>, dim3(ntiles, hkv), block, 0, st, part_o, part_lse,
-                               q_start, tiles, out, hq, hkv, nsplit, ntiles);
+                               q_start, tiles, out, hq, hkv, nsplit, ntiles, CHRONOS_GATE);
     }
 }
 

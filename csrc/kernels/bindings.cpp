@@ -19,6 +19,8 @@
 #include <vector>
 #include <cstring>
 
+#include "chronos_gemv.h"
+
 namespace chronos {
 void launch_embedding(const int32_t*, const uint16_t*, uint16_t*, int, int, int64_t, int64_t, hipStream_t);
 void launch_rmsnorm(const uint16_t*, uint16_t*, const uint16_t*, uint16_t*, int, int, float, hipStream_t);
@@ -51,6 +53,10 @@ void launch_qlinear(const uint8_t*, const float*, const uint8_t*, const float*, 
 }  // namespace chronos
 
 namespace chronos {
+// decode early-exit gate (chronos_hip.h): read by the launchers, baked into captured graphs as kernel arguments
+const int32_t* g_gate_state = nullptr;
+int g_gate_n = 0;
+
 namespace {
 std::mutex g_knob_mu;
 std::unordered_map<std::string, int> g_knobs;
@@ -296,6 +302,101 @@ Tensor gemv(const Tensor& x, const Tensor& w, bool swiglu) {
     return y;
 }
 
+// Decode gate: state = the engine's slot-state vector (int32, >= n rows); n in [1, 8] arms it for the launches that
+// follow, n = 0 disarms.  Only decode steps of a small bucket arm it (a prefill or a large bucket never does).
+void set_decode_gate(const c10::optional<Tensor>& state, int64_t n) {
+    if (!state.has_value() || n <= 0) {
+        chronos::g_gate_state = nullptr;
+        chronos::g_gate_n = 0;
+        return;
+    }
+    chk_i32(*state, "gate state");
+    CHK(n <= 8 && state->numel() >= n, "decode gate: 1 <= n <= 8 and n <= numel(state)");
+    chronos::g_gate_state = i32(*state);
+    chronos::g_gate_n = (int)n;
+}
+
+// Decode producer (O / down projection at TP=1, M <= 2): resid_out = bf16(bf16(x @ w.T) + resid_in); returns the
+// per-workgroup sums of resid_out^2 [M, P] f32 that the consuming GEMV's norm prologue reduces (chronos_gemv.h).
+Tensor gemv_resid(const Tensor& x, const Tensor& w, const Tensor& resid_in, const Tensor& resid_out) {
+    chk_bf16(x, "x");
+    chk_bf16(w, "w");
+    chk_bf16(resid_in, "resid_in");
+    chk_bf16(resid_out, "resid_out");
+    const int64_t K = x.size(-1), M = x.numel() / K, N = w.size(0);
+    CHK(w.dim() == 2 && w.size(1) == K, "gemv_resid: w must be [N, K]");
+    CHK(M >= 1 && M <= 2 && K % 512 == 0 && N % 16 == 0, "gemv_resid: M <= 2, K % 512, N % 16");
+    CHK(resid_in.numel() == M * N && resid_out.numel() == M * N, "gemv_resid: residuals must be [M, N]");
+    CHK(resid_in.data_ptr() != resid_out.data_ptr(), "gemv_resid: out of place only");
+    c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+    auto part = at::empty({M, chronos::gemv_resid_parts((int)M, (int)N)}, x.options().dtype(at::kFloat));
+    chronos::launch_gemv_resid(bf(x), (int)M, (int)K, bf(w), (int)N, bf(resid_in), bfm(resid_out),
+                               part.data_ptr<float>(), cur_stream());
+    return part;
+}
+
+inline chronos::GemvNorm normp_args(const Tensor& s, const Tensor& part, double eps, int64_t M) {
+    chk_gpu(part, "part");
+    CHK(part.scalar_type() == at::kFloat && part.dim() == 2 && part.size(0) == M, "part must be [M, P] f32");
+    CHK(part.size(1) % 4 == 0 && part.size(1) <= 1024, "part: P % 4 == 0, P <= 1024");
+    (void)s;
+    chronos::GemvNorm n{};
+    n.part = part.data_ptr<float>();
+    n.nparts = (int)part.size(1);
+    n.eps = (float)eps;
+    return n;
+}
+
+// Decode consumer: y = rmsnorm(s) @ w.T for a projection w whose norm weight is folded in (models/llama.py
+// fold_norm), the norm's sum of squares taken from a gemv_resid producer's partials (swiglu: gate/up pair ->
+// silu(g) * u).  s: [M, K], M <= 2.
+Tensor gemv_normp(const Tensor& s, const Tensor& part, double eps, const Tensor& w, bool swiglu) {
+    chk_bf16(s, "s");
+    chk_bf16(w, "w");
+    const int64_t K = s.size(-1), M = s.numel() / K, N = w.size(0);
+    CHK(w.dim() == 2 && w.size(1) == K, "gemv_normp: w must be [N, K]");
+    CHK(M >= 1 && M <= 2 && K % 512 == 0 && N % 16 == 0, "gemv_normp: M <= 2, K % 512, N % 16");
+    const chronos::GemvNorm n = normp_args(s, part, eps, M);
+    c10::hip::HIPGuardMasqueradingAsCUDA g(s.device());
+    auto y = at::empty({M, swiglu ? N / 2 : N}, s.options());
+    chronos::launch_gemv_ex(bf(s), (int)M, (int)K, bf(w), (int)N, bfm(y), swiglu, &n, nullptr, false, cur_stream());
+    return y;
+}
+
+// Decode QKV projection with the RoPE + paged-KV epilogue (rope_kv_write's semantics): q -> q_out, k/v -> the caches.
+// part given: x is the residual stream s and the (folded) input RMSNorm is fused as in gemv_normp; else x is the
+// normalised input.  M <= 2 tokens, token m belongs to block-table row tok_seq[m].
+void qkv_rope(const Tensor& x, const c10::optional<Tensor>& part, double eps,
+              const Tensor& w, const Tensor& pos, const Tensor& tok_seq, const Tensor& block_table,
+              const Tensor& cos_sin, const Tensor& q_out, const Tensor& k_cache, const Tensor& v_cache, int64_t hq,
+              int64_t hkv, double k_scale, double v_scale) {
+    chk_bf16(x, "x");
+    chk_bf16(w, "w");
+    chk_i32(pos, "pos");
+    chk_i32(tok_seq, "tok_seq");
+    chk_i32(block_table, "block_table");
+    chk_gpu(cos_sin, "cos_sin");
+    CHK(cos_sin.scalar_type() == at::kFloat && cos_sin.dim() == 2 && cos_sin.size(1) == 128, "cos_sin [P,128] f32");
+    chk_bf16(q_out, "q_out");
+    const bool fp8 = chk_kv(k_cache, v_cache);
+    const int64_t K = x.size(-1), M = x.numel() / K, N = w.size(0);
+    CHK(M >= 1 && M <= 2 && K % 512 == 0, "qkv_rope: M <= 2, K % 512 == 0");
+    CHK(w.dim() == 2 && w.size(1) == K && N == (hq + 2 * hkv) * 128, "w must be [(hq+2hkv)*128, K]");
+    CHK(pos.numel() >= M && tok_seq.numel() >= M && q_out.numel() >= M * hq * 128, "pos/tok_seq/q_out too small");
+    CHK(k_cache.dim() == 4 && k_cache.size(1) == hkv && k_cache.size(3) == 128, "k_cache [NB, hkv, BS, 128]");
+    CHK(v_cache.dim() == 4 && v_cache.size(1) == hkv && v_cache.size(2) == 128 && v_cache.size(3) == k_cache.size(2),
+        "v_cache [NB, hkv, 128, BS]");
+    CHK(block_table.dim() == 2, "block_table [B, max_blocks]");
+    chronos::GemvNorm n{};
+    if (part.has_value()) n = normp_args(x, *part, eps, M);
+    c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+    chronos::GemvRope rp{i32(pos), i32(tok_seq), i32(block_table), (int)block_table.size(1), cos_sin.data_ptr<float>(),
+                         bfm(q_out), k_cache.data_ptr(), v_cache.data_ptr(), (int)hq, (int)hkv, (int)k_cache.size(2),
+                         (float)(1.0 / k_scale), (float)(1.0 / v_scale)};
+    chronos::launch_gemv_ex(bf(x), (int)M, (int)K, bf(w), (int)N, nullptr, false, part.has_value() ? &n : nullptr,
+                            &rp, fp8, cur_stream());
+}
+
 // y = x @ w.T on MFMA (gemm.hip); swiglu as gemv.  stages = depth of the LDS-DMA ring (2..4)
 Tensor gemm(const Tensor& x, const Tensor& w, bool swiglu, int64_t stages) {
     chk_bf16(x, "x");
@@ -413,6 +514,12 @@ TORCH_LIBRARY(chronos, m) {
     m.def("silu_mul(Tensor gate_up) -> Tensor");
     m.def("gemv(Tensor x, Tensor w, bool swiglu) -> Tensor");
     m.def("gemm(Tensor x, Tensor w, bool swiglu, int stages=3) -> Tensor");
+    m.def("gemv_resid(Tensor x, Tensor w, Tensor resid_in, Tensor(a!) resid_out) -> Tensor");
+    m.def("gemv_normp(Tensor s, Tensor part, float eps, Tensor w, bool swiglu) -> Tensor");
+    m.def("qkv_rope(Tensor x, Tensor? part, float eps, Tensor w, Tensor pos, Tensor tok_seq, "
+          "Tensor block_table, Tensor cos_sin, Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, int hq, "
+          "int hkv, float k_scale=1.0, float v_scale=1.0) -> ()");
+    m.def("set_decode_gate(Tensor? state, int n) -> ()", &set_decode_gate);
     m.def("quant_rows(Tensor x, Tensor(a!)? resid, Tensor? w, float eps, int mode) -> (Tensor, Tensor)");
     m.def("qlinear(Tensor xq, Tensor xs, Tensor wq, Tensor ws, bool swiglu) -> Tensor");
     m.def("set_knob(str name, int value) -> ()", &set_knob);
@@ -439,6 +546,9 @@ TORCH_LIBRARY_IMPL(chronos, CUDA, m) {
     m.impl("silu_mul", &silu_mul);
     m.impl("gemv", &gemv);
     m.impl("gemm", &gemm);
+    m.impl("gemv_resid", &gemv_resid);
+    m.impl("gemv_normp", &gemv_normp);
+    m.impl("qkv_rope", &qkv_rope);
     m.impl("quant_rows", &quant_rows);
     m.impl("qlinear", &qlinear);
     m.impl("paged_attention", &paged_attention);

@@ -14,7 +14,9 @@ namespace chronos {
 // zero rows of a vocab-parallel shard are summed away by the TP all-reduce).
 // ------------------------------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) embedding_kernel(const int32_t* __restrict__ ids, const uint16_t* __restrict__ table,
-                                                        uint16_t* __restrict__ out, int d, int64_t vstart, int64_t vrows) {
+                                                        uint16_t* __restrict__ out, int d, int64_t vstart, int64_t vrows,
+                                                        const int32_t* __restrict__ gst, int gn) {
+    if (gate_closed(gst, gn)) return;
     const int t = blockIdx.x;
     const int64_t id = (int64_t)ids[t] - vstart;
     const bool ok = id >= 0 && id < vrows;
@@ -35,8 +37,9 @@ __global__ void __launch_bounds__(256) embedding_kernel(const int32_t* __restric
 template <int MAXV, bool RESID>
 __global__ void __launch_bounds__(256) rmsnorm_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ resid,
                                                       const uint16_t* __restrict__ w, uint16_t* __restrict__ y, int d,
-                                                      float eps) {
+                                                      float eps, const int32_t* __restrict__ gst, int gn) {
     __shared__ float red[16];
+    if (gate_closed(gst, gn)) return;
     const int64_t row = blockIdx.x;
     const u16x8* xv = reinterpret_cast<const u16x8*>(x + row * d);
     u16x8* rv = reinterpret_cast<u16x8*>(resid + row * d);
@@ -100,8 +103,9 @@ __global__ void __launch_bounds__(256) rope_kv_write_kernel(
     const uint16_t* __restrict__ qkv, const int32_t* __restrict__ pos, const int32_t* __restrict__ tok_seq,
     const int32_t* __restrict__ block_table, int bt_stride, const float* __restrict__ cos_sin,
     uint16_t* __restrict__ q_out, void* __restrict__ k_cache, void* __restrict__ v_cache, int hq, int hkv,
-    int block_size, int write_q, float k_inv_scale, float v_inv_scale) {
+    int block_size, int write_q, float k_inv_scale, float v_inv_scale, const int32_t* __restrict__ gst, int gn) {
     constexpr int D = 128;
+    if (gate_closed(gst, gn)) return;
     const int t = blockIdx.x;
     const int g = blockIdx.y * 256 + threadIdx.x;
     const int nh = hq + 2 * hkv;
@@ -201,7 +205,7 @@ __global__ void __launch_bounds__(256) silu_mul_kernel(const uint16_t* __restric
 void launch_embedding(const int32_t* ids, const uint16_t* table, uint16_t* out, int t, int d, int64_t vstart,
                       int64_t vrows, hipStream_t st) {
     if (t == 0) return;
-    hipLaunchKernelGGL(embedding_kernel, dim3(t), dim3(256), 0, st, ids, table, out, d, vstart, vrows);
+    hipLaunchKernelGGL(embedding_kernel, dim3(t), dim3(256), 0, st, ids, table, out, d, vstart, vrows, CHRONOS_GATE);
 }
 
 void launch_rmsnorm(const uint16_t* x, uint16_t* resid, const uint16_t* w, uint16_t* y, int rows, int d, float eps,
@@ -211,8 +215,10 @@ void launch_rmsnorm(const uint16_t* x, uint16_t* resid, const uint16_t* w, uint1
     const dim3 g(rows), b(256);
 #define RMS_CASE(V)                                                                                         \
     if (nv <= 256 * V) {                                                                                    \
-        if (resid) hipLaunchKernelGGL((rmsnorm_kernel<V, true>), g, b, 0, st, x, resid, w, y, d, eps);       \
-        else hipLaunchKernelGGL((rmsnorm_kernel<V, false>), g, b, 0, st, x, resid, w, y, d, eps);           \
+        if (resid)                                                                                          \
+            hipLaunchKernelGGL((rmsnorm_kernel<V, true>), g, b, 0, st, x, resid, w, y, d, eps, CHRONOS_GATE);  \
+        else                                                                                                \
+            hipLaunchKernelGGL((rmsnorm_kernel<V, false>), g, b, 0, st, x, resid, w, y, d, eps, CHRONOS_GATE); \
         return;                                                                                             \
     }
     RMS_CASE(1) RMS_CASE(2) RMS_CASE(4) RMS_CASE(8)
@@ -227,10 +233,11 @@ void launch_rope_kv_write(const uint16_t* qkv, const int32_t* pos, const int32_t
     const dim3 g(t, (8 * (hq + hkv) + 64 * hkv + 255) / 256), b(256);
     if (fp8)
         hipLaunchKernelGGL(rope_kv_write_kernel<true>, g, b, 0, st, qkv, pos, tok_seq, block_table, bt_stride, cos_sin,
-                           q_out, k_cache, v_cache, hq, hkv, block_size, write_q, 1.f / k_scale, 1.f / v_scale);
+                           q_out, k_cache, v_cache, hq, hkv, block_size, write_q, 1.f / k_scale, 1.f / v_scale,
+                           CHRONOS_GATE);
     else
         hipLaunchKernelGGL(rope_kv_write_kernel<false>, g, b, 0, st, qkv, pos, tok_seq, block_table, bt_stride,
-                           cos_sin, q_out, k_cache, v_cache, hq, hkv, block_size, write_q, 1.f, 1.f);
+                           cos_sin, q_out, k_cache, v_cache, hq, hkv, block_size, write_q, 1.f, 1.f, CHRONOS_GATE);
 }
 
 void launch_silu_mul(const uint16_t* gu, uint16_t* out, int64_t rows, int f, hipStream_t st) {

@@ -48,8 +48,10 @@ __device__ __forceinline__ bf16x8 lds_frag(const unsigned char* img, int row, in
 
 template <int STAGES, bool SWIGLU>
 __global__ void __launch_bounds__(256) gemm_bf16_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
-                                                        uint16_t* __restrict__ y, int M, int N, int K, int F) {
+                                                        uint16_t* __restrict__ y, int M, int N, int K, int F,
+                                                        const int32_t* __restrict__ gst, int gn) {
     extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];  // STAGES x {W image, x image}
+    if (gate_closed(gst, gn)) return;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int mt = (M + BM - 1) / BM;
     const int nt = (SWIGLU ? F / 64 : N / BN);
@@ -172,7 +174,8 @@ void launch_stages(const uint16_t* x, const uint16_t* w, uint16_t* y, int M, int
                             hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         attr = true;
     }
-    hipLaunchKernelGGL((gemm_bf16_kernel<STAGES, SWIGLU>), dim3(mt * nt), dim3(256), lds, st, x, w, y, M, N, K, F);
+    hipLaunchKernelGGL((gemm_bf16_kernel<STAGES, SWIGLU>), dim3(mt * nt), dim3(256), lds, st, x, w, y, M, N, K, F,
+                       CHRONOS_GATE);
 }
 
 }  // namespace

@@ -15,6 +15,7 @@
 // One 256-thread workgroup owns R output rows.  Fused SwiGLU epilogue for the gate/up projection (w = [gate; up]):
 // the workgroup streams R gate rows and the matching R up rows and writes silu(g) * u directly.
 #include "chronos_hip.h"
+#include "chronos_gemv.h"
 
 namespace chronos {
 
@@ -40,10 +41,28 @@ __device__ __forceinline__ float dot8(const u16x8& w, const u16x8& x, float acc)
     return acc;
 }
 
-template <int M, int R, bool SWIGLU>
+// Fused decode-step variants (M <= 2 rows: one sensor stream or two), chronos_gemv.h:
+//   * kResid epilogue (O / down projection, TP=1): instead of y, write the new residual s = bf16(bf16(y) + r) and the
+//     workgroup's per-row sum of s^2 — the producer half of the next RMSNorm;
+//   * NORMP (QKV / gate_up / LM head): x is the raw residual stream s.  The norm weight is folded into the projection
+//     weights at load time (W' = W diag(w), models/llama.py), so rmsnorm(s) w @ W^T = inv * (s @ W'^T) with
+//     inv = rsqrt(sum of the producer's partials / K + eps): the prologue reduces the partials per wave (no barrier,
+//     fixed order) and the epilogue scales the row sums by inv — no norm launch, no per-element work, no extra
+//     bytes over the plain GEMV;
+//   * ROPE epilogue (QKV): workgroup b owns dims {4j..4j+3} and {64+4j..64+4j+3} of head b/16 (j = b%16) — the
+//     rotate-half pairs — so it applies RoPE and writes q to q_out and k, v straight into the paged cache (bf16 or
+//     fp8-e4m3), exactly as rope_kv_write_kernel does from the bf16 qkv output.
+// Together they take a TP=1 decode layer from 9 launches (norm, qkv, rope, attn, combine, o, norm, gate_up, down) to 6.
+enum : int { kPlain = 0, kSwiglu = 1, kRope = 2, kRope8 = 3, kResid = 4 };
+
+template <int M, int R, int MODE, bool NORMP>
 __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ x, int mrows, int K,
                                                    const uint16_t* __restrict__ W, uint16_t* __restrict__ y,
-                                                   int nout, int half) {
+                                                   int nout, int half, GemvNorm nrm, GemvRope rp,
+                                                   const int32_t* __restrict__ gst, int gn) {
+    constexpr bool SWIGLU = MODE == kSwiglu;
+    constexpr bool ROPE = MODE == kRope || MODE == kRope8;
+    static_assert(!ROPE || R == 8, "rope epilogue: 4 rotate-half pairs per workgroup");
     constexpr int NR = SWIGLU ? 2 * R : R;  // weight rows streamed by this workgroup
     constexpr int V = NR * M;               // partial sums per lane
     constexpr int DEPTH = (NR + M) * 4 <= 40 ? 3 : 2;  // register ring depth (VGPR budget)
@@ -55,7 +74,9 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
     const u16x8* wrow[NR];
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
-        const int row = (SWIGLU && r >= R) ? half + n0 + (r - R) : n0 + r;
+        int row;
+        if constexpr (ROPE) row = (blockIdx.x >> 4) * 128 + (r < 4 ? 0 : 64) + 4 * (blockIdx.x & 15) + (r & 3);
+        else row = (SWIGLU && r >= R) ? half + n0 + (r - R) : n0 + r;
         wrow[r] = reinterpret_cast<const u16x8*>(W + (int64_t)row * K);
     }
     const u16x8* xr = reinterpret_cast<const u16x8*>(x);
@@ -65,17 +86,46 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
 #pragma unroll
     for (int i = 0; i < V; ++i) acc[i] = 0.f;
     u16x8 wr[DEPTH][NR], xv[DEPTH][M];
-    auto load = [&](int c, u16x8 (&wd)[NR], u16x8 (&xd)[M]) {
+    auto load = [&](int c, int d) {
         const int off = c * 64 + lane;
 #pragma unroll
-        for (int r = 0; r < NR; ++r) wd[r] = ld_nt(wrow[r] + off);
+        for (int r = 0; r < NR; ++r) wr[d][r] = ld_nt(wrow[r] + off);
 #pragma unroll
-        for (int m = 0; m < M; ++m) xd[m] = m < mrows ? xr[m * xstride + off] : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        for (int m = 0; m < M; ++m) xv[d][m] = m < mrows ? xr[m * xstride + off] : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
     };
+    // NORMP: the producer's partials (<= 1024 per row) are fetched FIRST, as up to 4 float4 per lane all in flight, so
+    // the reduction below waits only for them (vmcnt is in order) and never for the weight ring issued after them
+    float4 pv[M][4];
+    if constexpr (NORMP) {
+#pragma unroll
+        for (int m = 0; m < M; ++m)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int i = (q * 64 + lane) * 4;
+                pv[m][q] = (m < mrows && i < nrm.nparts)
+                               ? *reinterpret_cast<const float4*>(nrm.part + m * nrm.nparts + i)
+                               : float4{0.f, 0.f, 0.f, 0.f};
+            }
+    }
     // wave w takes chunks w, w+4, w+8, ...
 #pragma unroll
     for (int d = 0; d < DEPTH; ++d)
-        if (w + 4 * d < nchunk) load(w + 4 * d, wr[d], xv[d]);
+        if (w + 4 * d < nchunk) load(w + 4 * d, d);
+    // the decode gate is checked with the first loads already in flight (a closed gate only wastes their bandwidth)
+    if (gate_closed(gst, gn)) return;
+    float inv[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) inv[m] = 1.f;
+    if constexpr (NORMP) {
+        // every wave reduces the partials itself in the same fixed order: no barrier, identical inv in all waves
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            float ss = 0.f;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) ss += (pv[m][q].x + pv[m][q].y) + (pv[m][q].z + pv[m][q].w);
+            inv[m] = rsqrtf(wave_sum(ss) / (float)K + nrm.eps);
+        }
+    }
     for (int c0 = w; c0 < nchunk; c0 += 4 * DEPTH) {
 #pragma unroll
         for (int d = 0; d < DEPTH; ++d) {
@@ -85,7 +135,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
                 for (int r = 0; r < NR; ++r)
 #pragma unroll
                     for (int m = 0; m < M; ++m) acc[r * M + m] = dot8(wr[d][r], xv[d][m], acc[r * M + m]);
-                if (c + 4 * DEPTH < nchunk) load(c + 4 * DEPTH, wr[d], xv[d]);
+                if (c + 4 * DEPTH < nchunk) load(c + 4 * DEPTH, d);
             }
         }
     }
@@ -95,13 +145,87 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
         if (lane == 0) red[w][i] = s;
     }
     __syncthreads();
+    // row sums (NORMP: times the row's inv — the folded RMSNorm; 1 otherwise)
+    auto invm = [&](int m) {  // select chain: a runtime index into inv[] would put it in scratch
+        float v = inv[0];
+#pragma unroll
+        for (int j = 1; j < M; ++j) v = m == j ? inv[j] : v;
+        return v;
+    };
+    auto tot = [&](int i) { return (red[0][i] + red[1][i] + red[2][i] + red[3][i]) * invm(i % M); };
+    if constexpr (ROPE) {
+        // thread t < 4*M: pair (r, r+4) of row m; the unfused path rounds the GEMM output to bf16 before RoPE
+        const int t = threadIdx.x;
+        if (t >= 4 * M) return;
+        const int pr = t / M, m = t % M;
+        if (m >= mrows) return;
+        const int unit = blockIdx.x >> 4, d = 4 * (blockIdx.x & 15) + pr;  // head (q | k | v) and dim in [0, 64)
+        const float x1 = bf2f(f2bf(tot(pr * M + m))), x2 = bf2f(f2bf(tot((pr + 4) * M + m)));
+        const int p = rp.pos[m];
+        const int64_t blk = rp.bt[(int64_t)rp.tok_seq[m] * rp.bt_stride + p / rp.bs];
+        const int off = p % rp.bs;
+        if (unit < rp.hq + rp.hkv) {
+            const float c = rp.cos_sin[(int64_t)p * 128 + d], sn = rp.cos_sin[(int64_t)p * 128 + 64 + d];
+            const float fa = x1 * c - x2 * sn, fb = x2 * c + x1 * sn;
+            if (unit < rp.hq) {
+                uint16_t* dst = rp.q_out + ((int64_t)m * rp.hq + unit) * 128;
+                dst[d] = f2bf(fa);
+                dst[64 + d] = f2bf(fb);
+            } else if constexpr (MODE == kRope8) {
+                uint8_t* dst = reinterpret_cast<uint8_t*>(rp.kc) + ((blk * rp.hkv + (unit - rp.hq)) * rp.bs + off) * 128;
+                const uint32_t q = f32x4_to_fp8x4(fa * rp.k_inv, fb * rp.k_inv, 0.f, 0.f);
+                dst[d] = (uint8_t)q;
+                dst[64 + d] = (uint8_t)(q >> 8);
+            } else {
+                uint16_t* dst = reinterpret_cast<uint16_t*>(rp.kc) + ((blk * rp.hkv + (unit - rp.hq)) * rp.bs + off) * 128;
+                dst[d] = f2bf(fa);
+                dst[64 + d] = f2bf(fb);
+            }
+        } else {  // v: transposed [blk, h, dim, slot]
+            const int64_t base = ((blk * rp.hkv + (unit - rp.hq - rp.hkv)) * 128) * (int64_t)rp.bs + off;
+            if constexpr (MODE == kRope8) {
+                uint8_t* dst = reinterpret_cast<uint8_t*>(rp.vc) + base;
+                const uint32_t q = f32x4_to_fp8x4(x1 * rp.v_inv, x2 * rp.v_inv, 0.f, 0.f);
+                dst[(int64_t)d * rp.bs] = (uint8_t)q;
+                dst[(int64_t)(64 + d) * rp.bs] = (uint8_t)(q >> 8);
+            } else {
+                uint16_t* dst = reinterpret_cast<uint16_t*>(rp.vc) + base;
+                dst[(int64_t)d * rp.bs] = f2bf(x1);
+                dst[(int64_t)(64 + d) * rp.bs] = f2bf(x2);
+            }
+        }
+        return;
+    }
+    if constexpr (MODE == kResid) {
+        // s = bf16(bf16(y) + r) -> rout; per-row sum of s^2 over this workgroup's R outputs -> part_out (fixed order)
+        __shared__ float sq[R * M];
+        const int t = threadIdx.x;
+        if (t < R * M) {
+            const int r = t / M, m = t % M;
+            float v = 0.f;
+            if (m < mrows) {
+                const int64_t i = (int64_t)m * nout + n0 + r;
+                const uint16_t sb = f2bf(bf2f(f2bf(tot(t))) + bf2f(nrm.rin[i]));
+                nrm.rout[i] = sb;
+                v = bf2f(sb) * bf2f(sb);
+            }
+            sq[t] = v;
+        }
+        __syncthreads();
+        if (t < M && t < mrows) {
+            float ss = 0.f;
+#pragma unroll
+            for (int r = 0; r < R; ++r) ss += sq[r * M + t];
+            nrm.part_out[t * gridDim.x + blockIdx.x] = ss;
+        }
+        return;
+    }
     for (int t = threadIdx.x; t < R * M; t += 256) {
         const int r = t / M, m = t % M;
         if (m >= mrows) continue;
-        const float g = red[0][r * M + m] + red[1][r * M + m] + red[2][r * M + m] + red[3][r * M + m];
+        const float g = tot(r * M + m);
         if constexpr (SWIGLU) {
-            const int ru = (R + r) * M + m;
-            const float u = red[0][ru] + red[1][ru] + red[2][ru] + red[3][ru];
+            const float u = tot((R + r) * M + m);
             const float gb = bf2f(f2bf(g)), ub = bf2f(f2bf(u));  // the unfused path rounds the GEMM outputs
             const float sg = bf2f(f2bf(gb / (1.f + __expf(-gb))));
             y[(int64_t)m * nout + n0 + r] = f2bf(sg * ub);
@@ -111,28 +235,75 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
     }
 }
 
+// R rows per workgroup: as many as the in-wave reduce-scatter (<= 64 sums per lane) allows, so x (re-read from L2 per
+// chunk) stays a small fraction of the weight bytes.
 template <int M>
-static void launch_m(const uint16_t* x, int mrows, int K, const uint16_t* W, int N, uint16_t* y, bool swiglu,
-                     hipStream_t st) {
-    // R rows per workgroup: as many as the in-wave reduce-scatter (<= 64 sums per lane) allows, so x (re-read from L2
-    // per chunk) stays a small fraction of the weight bytes.
-    constexpr int R1 = M <= 2 ? 8 : 4;
-    constexpr int R2 = M <= 2 ? 4 : 2;
-    if (swiglu) {
+constexpr int rows_plain() { return M <= 2 ? 8 : 4; }
+template <int M>
+constexpr int rows_swiglu() { return M <= 2 ? 4 : 2; }
+
+template <int M>
+static void launch_m(const uint16_t* x, int mrows, int K, const uint16_t* W, int N, uint16_t* y, int mode,
+                     const GemvNorm* nrm, const GemvRope* rp, hipStream_t st) {
+    constexpr int R1 = rows_plain<M>(), R2 = rows_swiglu<M>();
+    const GemvNorm nz{};
+    const GemvRope rz{};
+    const GemvNorm na = nrm ? *nrm : nz;
+    const GemvRope ra = rp ? *rp : rz;
+    const bool np = nrm && nrm->part;  // consumer of a kResid producer
+#define GV(MODE_, NP_, RR, GRID, NOUT, HALF)                                                                     \
+    hipLaunchKernelGGL((gemv_kernel<M, RR, MODE_, NP_>), dim3(GRID), dim3(256), 0, st, x, mrows, K, W, y, NOUT, \
+                       HALF, na, ra, CHRONOS_GATE)
+    if (mode == kSwiglu) {
         const int F = N / 2;
-        hipLaunchKernelGGL((gemv_kernel<M, R2, true>), dim3(F / R2), dim3(256), 0, st, x, mrows, K, W, y, F, F);
-    } else {
-        hipLaunchKernelGGL((gemv_kernel<M, R1, false>), dim3(N / R1), dim3(256), 0, st, x, mrows, K, W, y, N, 0);
+        if (np) GV(kSwiglu, true, R2, F / R2, F, F);
+        else GV(kSwiglu, false, R2, F / R2, F, F);
+    } else if (mode == kPlain) {
+        if (np) GV(kPlain, true, R1, N / R1, N, 0);
+        else GV(kPlain, false, R1, N / R1, N, 0);
+    } else if constexpr (M <= 2) {
+        if (mode == kResid) GV(kResid, false, R1, N / R1, N, 0);
+        else if (mode == kRope) {
+            if (np) GV(kRope, true, 8, N / 8, N, 0);
+            else GV(kRope, false, 8, N / 8, N, 0);
+        } else {
+            if (np) GV(kRope8, true, 8, N / 8, N, 0);
+            else GV(kRope8, false, 8, N / 8, N, 0);
+        }
     }
+#undef GV
 }
 
 void launch_gemv(const uint16_t* x, int M, int K, const uint16_t* W, int N, uint16_t* y, bool swiglu,
                  hipStream_t st) {
     if (M <= 0) return;
-    if (M == 1) launch_m<1>(x, M, K, W, N, y, swiglu, st);
-    else if (M == 2) launch_m<2>(x, M, K, W, N, y, swiglu, st);
-    else if (M <= 4) launch_m<4>(x, M, K, W, N, y, swiglu, st);
-    else launch_m<8>(x, M, K, W, N, y, swiglu, st);
+    const int mode = swiglu ? kSwiglu : kPlain;
+    if (M == 1) launch_m<1>(x, M, K, W, N, y, mode, nullptr, nullptr, st);
+    else if (M == 2) launch_m<2>(x, M, K, W, N, y, mode, nullptr, nullptr, st);
+    else if (M <= 4) launch_m<4>(x, M, K, W, N, y, mode, nullptr, nullptr, st);
+    else launch_m<8>(x, M, K, W, N, y, mode, nullptr, nullptr, st);
+}
+
+void launch_gemv_ex(const uint16_t* x, int M, int K, const uint16_t* W, int N, uint16_t* y, bool swiglu,
+                    const GemvNorm* nrm, const GemvRope* rope, bool fp8, hipStream_t st) {
+    if (M <= 0) return;
+    const int mode = rope ? (fp8 ? kRope8 : kRope) : swiglu ? kSwiglu : kPlain;
+    if (M == 1) launch_m<1>(x, M, K, W, N, y, mode, nrm, rope, st);
+    else launch_m<2>(x, M, K, W, N, y, mode, nrm, rope, st);
+}
+
+int gemv_resid_parts(int M, int N) { return N / (M <= 2 ? rows_plain<1>() : rows_plain<4>()); }
+
+int launch_gemv_resid(const uint16_t* x, int M, int K, const uint16_t* W, int N, const uint16_t* rin, uint16_t* rout,
+                      float* part_out, hipStream_t st) {
+    if (M <= 0) return 0;
+    GemvNorm nrm{};
+    nrm.rin = rin;
+    nrm.rout = rout;
+    nrm.part_out = part_out;
+    if (M == 1) launch_m<1>(x, M, K, W, N, nullptr, kResid, &nrm, nullptr, st);
+    else launch_m<2>(x, M, K, W, N, nullptr, kResid, &nrm, nullptr, st);
+    return gemv_resid_parts(M, N);
 }
 
 }  // namespace chronos

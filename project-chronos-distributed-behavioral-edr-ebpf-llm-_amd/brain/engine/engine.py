@@ -25,6 +25,7 @@ import collections
 import itertools
 import logging
 import math
+import os
 import threading
 import time
 from dataclasses import dataclass, field
@@ -41,6 +42,7 @@ from ..tokenizer import load_tokenizer
 from .block_manager import BlockManager
 
 log = logging.getLogger("chronos.engine")
+_PHASE_SYNC = os.environ.get("CHRONOS_PHASE_SYNC", "0") not in ("", "0")
 
 
 @dataclass
@@ -72,6 +74,7 @@ class EngineConfig:
     request_timeout_s: float = 0.0  # >0: a request not finished this long after submit is cancelled (reason "timeout")
     tp_overlap: bool = True        # TP prefill: two micro-batches, each one's RCCL all-reduces overlap the other's compute
     tp_overlap_min_tokens: int = 1024
+    decode_gate: bool = True       # small buckets: kernels of steps after the last live row finished return at once
 
 
 @dataclass
@@ -196,6 +199,8 @@ class Engine:
         self._graphs: dict[int, torch.cuda.CUDAGraph] = {}
         self._graph_pool = None
         self.stats = collections.Counter()
+        # host wall seconds per scheduler phase (harvest includes harvest_gpu_wait: the wait for the burst to finish)
+        self.phase_s: collections.Counter = collections.Counter()
         # re-entrant: request callbacks run on the scheduler thread and may submit follow-up requests (closed loop)
         self._lock = threading.RLock()
         self._cancels: list[tuple[Request, str]] = []
@@ -261,16 +266,25 @@ class Engine:
         A prefill step never syncs: its first tokens are sampled on device and a request that finishes on them is
         harvested after the next burst.  A decode burst queues its own snapshot and (async mode) harvests the previous
         one, which completed as soon as the GPU started on this burst."""
+        pc, ph = time.perf_counter, self.phase_s
+        t0 = pc()
         reaped = self._reap()
         with trace.range("admit"):
             self._admit()
+        t1 = pc()
+        ph["admit"] += t1 - t0
         if self.prefilling:
             with trace.range("prefill"):
                 self._prefill_step()
+            if _PHASE_SYNC and self.device.type == "cuda":
+                torch.cuda.synchronize()  # attribute the prefill's GPU time to it (diagnostics only)
+            ph["prefill_host"] += pc() - t1
             return reaped
         if self.running:
             with trace.range("decode_burst"):
                 snap = self._decode_burst()
+            t2 = pc()
+            ph["decode_launch"] += t2 - t1
             if not self._async:
                 prev = snap
             else:
@@ -278,7 +292,9 @@ class Engine:
             if prev is None:
                 return reaped
             with trace.range("harvest"):
-                return reaped + self._harvest(prev)
+                out = reaped + self._harvest(prev)
+            ph["harvest"] += pc() - t2
+            return out
         self._pending = None
         return reaped
 
@@ -461,9 +477,14 @@ class Engine:
                 g = self._capture(n)
             g.replay()
         else:
-            for _ in range(k):
-                self._decode_once(n, self._nsplit(n))
+            self._gate(n)
+            try:
+                for _ in range(k):
+                    self._decode_once(n, self._nsplit(n))
+            finally:
+                self._gate(0)
         self.stats["decode_steps"] += k
+        self.stats[f"bursts@{n}"] += 1
         self.stats["decode_row_steps"] += k * n
         return self._snapshot(n)
 
@@ -479,15 +500,25 @@ class Engine:
             ev.record()
         return _Snapshot(n, ev, st, no, out, dict(self.running))
 
+    def _gate(self, n: int) -> None:
+        """Arm the decode early-exit gate for a small bucket (n <= 8 rows): the steps of a burst after every row's
+        verdict closed skip all their kernels (csrc/include/chronos_hip.h).  Relies on DONE == 0, empty == -1."""
+        if self.device.type == "cuda" and self.cfg.decode_gate:
+            ops.set_decode_gate(self.s_state, n if 0 < n <= 8 else 0)
+
     def _capture(self, n: int) -> "torch.cuda.CUDAGraph":
         if self._graph_pool is None:
             self._graph_pool = torch.cuda.graph_pool_handle()
         g = torch.cuda.CUDAGraph()
         ns = self._nsplit(n)
         torch.cuda.synchronize()
-        with torch.cuda.graph(g, pool=self._graph_pool):
-            for _ in range(self.cfg.decode_burst):
-                self._decode_once(n, ns)
+        self._gate(n)
+        try:
+            with torch.cuda.graph(g, pool=self._graph_pool):
+                for _ in range(self.cfg.decode_burst):
+                    self._decode_once(n, ns)
+        finally:
+            self._gate(0)
         self._graphs[n] = g
         self.stats["graphs_captured"] += 1
         return g
@@ -501,7 +532,9 @@ class Engine:
 
     def _harvest(self, snap: _Snapshot) -> list[Request]:
         if snap.event is not None:
+            t = time.perf_counter()
             snap.event.synchronize()
+            self.phase_s["harvest_gpu_wait"] += time.perf_counter() - t
         # (snapshot slot, request) for requests still running as the same object (identity, not slot number)
         live = [(s, r) for s, r in snap.owners.items() if self.running.get(r.slot) is r]
         if not live:

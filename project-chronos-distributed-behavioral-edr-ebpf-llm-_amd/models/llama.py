@@ -25,6 +25,10 @@ import torch
 from .. import ops
 from ..parallel.tp import TPContext
 
+# decode steps (T <= 2, TP=1): residual add + norm partials in the producing GEMV's epilogue, the norm in the consuming
+# GEMV's prologue, RoPE + paged-KV write in the QKV GEMV's epilogue (CHRONOS_FUSE_NORM=0: the separate kernels)
+_FUSE_NORM = os.environ.get("CHRONOS_FUSE_NORM", "1") != "0"
+
 
 @dataclass
 class LlamaConfig:
@@ -190,6 +194,9 @@ class LlamaWeights:
     norm: torch.Tensor
     lm_head: torch.Tensor          # [V_local, d]
     vocab_start: int = 0
+    # RMSNorm weights folded into the following projections (W' = W diag(w), norms stored as ones): what the decode
+    # GEMV's folded-norm prologue (csrc/kernels/gemv.hip NORMP) relies on
+    norms_folded: bool = False
 
     def nbytes(self) -> int:
         n = 2 * (self.embed.numel() + self.norm.numel() + (0 if self.lm_head is self.embed else self.lm_head.numel()))
@@ -219,10 +226,28 @@ def _local_heads(cfg: LlamaConfig, tp: TPContext) -> tuple[int, int]:
     return cfg.num_heads // tp.world, cfg.num_kv_heads // tp.world
 
 
+def fold_norm(wt: torch.Tensor, nw: torch.Tensor) -> torch.Tensor:
+    """W diag(nw): an RMSNorm weight folded into the projection that consumes the norm (scales W's input columns, one
+    bf16 rounding).  rmsnorm(x) * nw @ W^T == rmsnorm(x) @ (W diag(nw))^T.  A ones vector (random init) is a no-op."""
+    if bool((nw == 1).all()):
+        return wt
+    return (wt.float() * nw.float().to(wt.device)).to(wt.dtype)
+
+
 def assemble_layer(cfg: LlamaConfig, tp: TPContext, full: dict, device, dtype=torch.bfloat16,
-                   weight_dtype: str = "bf16") -> LayerWeights:
+                   weight_dtype: str = "bf16", fold_norms: bool = True) -> LayerWeights:
     """Full (unsharded) HF-named tensors of one layer -> this rank's fused shard (projections quantised to
-    per-channel e4m3 when ``weight_dtype == "fp8"``; norms stay bf16)."""
+    per-channel e4m3 when ``weight_dtype == "fp8"``; norms stay bf16).  ``fold_norms``: the input-norm weights are
+    folded into QKV / gate_up (before quantisation) and stored as ones."""
+    if fold_norms:
+        full = dict(full)
+        an, mn = full["attn_norm"], full["mlp_norm"]
+        for n in ("q", "k", "v"):
+            full[n] = fold_norm(full[n], an)
+        for n in ("gate", "up"):
+            full[n] = fold_norm(full[n], mn)
+        full["attn_norm"] = torch.ones_like(an)
+        full["mlp_norm"] = torch.ones_like(mn)
     r, w = tp.rank, tp.world
     D = cfg.head_dim
     q = full["q"].view(cfg.num_heads, D, -1)
@@ -247,7 +272,7 @@ def assemble_layer(cfg: LlamaConfig, tp: TPContext, full: dict, device, dtype=to
 
 
 def random_weights(cfg: LlamaConfig, tp: TPContext | None = None, device="cpu", seed: int = 0,
-                   dtype=torch.bfloat16, weight_dtype: str = "bf16") -> LlamaWeights:
+                   dtype=torch.bfloat16, weight_dtype: str = "bf16", fold_norms: bool = True) -> LlamaWeights:
     """Random-init weights with the real architecture (the benchmark's model; no checkpoints offline).
 
     Every rank draws the FULL tensor from the same seeded generator and keeps its shard, so a TP run is numerically
@@ -281,7 +306,7 @@ def random_weights(cfg: LlamaConfig, tp: TPContext | None = None, device="cpu", 
             o=rnd(d, cfg.num_heads * D), mlp_norm=ones(d),
             gate=rnd(f, d), up=rnd(f, d), down=rnd(d, f),
         )
-        layers.append(assemble_layer(cfg, tp, full, dev, dtype, weight_dtype))
+        layers.append(assemble_layer(cfg, tp, full, dev, dtype, weight_dtype, fold_norms))
         del full
     gen.manual_seed(seed * 1000003 + 999983)
     if cfg.tie_word_embeddings:
@@ -290,7 +315,7 @@ def random_weights(cfg: LlamaConfig, tp: TPContext | None = None, device="cpu", 
         lm_full = rnd(cfg.vocab_size, d)
         lm_head = lm_full[tp.rank * vs:(tp.rank + 1) * vs].contiguous()
         del lm_full
-    return LlamaWeights(embed, layers, ones(d), lm_head, vocab_start=tp.rank * vs)
+    return LlamaWeights(embed, layers, ones(d), lm_head, vocab_start=tp.rank * vs, norms_folded=fold_norms)
 
 
 # ---- checkpoint loaders ----------------------------------------------------------------------------------------
@@ -302,8 +327,15 @@ def _meta_permute(w: torch.Tensor, n_heads: int) -> torch.Tensor:
     return w.view(n_heads, d1 // n_heads // 2, 2, d2).transpose(1, 2).reshape(d1, d2)
 
 
+def _final(norm: torch.Tensor, lm_head: torch.Tensor, fold: bool):
+    """(norm, lm_head) with the final norm folded into the LM head (a tied head becomes its own copy)."""
+    if not fold:
+        return norm, lm_head
+    return torch.ones_like(norm), fold_norm(lm_head, norm)
+
+
 def load_hf(path: str, tp: TPContext | None = None, device="cpu", dtype=torch.bfloat16,
-            weight_dtype: str = "bf16") -> tuple[LlamaConfig, LlamaWeights]:
+            weight_dtype: str = "bf16", fold_norms: bool = True) -> tuple[LlamaConfig, LlamaWeights]:
     """HF layout: config.json + model*.safetensors (tensor names: SURVEY.md App. B)."""
     from safetensors import safe_open
 
@@ -337,17 +369,18 @@ def load_hf(path: str, tp: TPContext | None = None, device="cpu", dtype=torch.bf
             v=get(p + "self_attn.v_proj.weight"), o=get(p + "self_attn.o_proj.weight"),
             gate=get(p + "mlp.gate_proj.weight"), up=get(p + "mlp.up_proj.weight"), down=get(p + "mlp.down_proj.weight"),
         )
-        layers.append(assemble_layer(cfg, tp, full, device, dtype, weight_dtype))
+        layers.append(assemble_layer(cfg, tp, full, device, dtype, weight_dtype, fold_norms))
     norm = get("model.norm.weight").to(device=device, dtype=dtype)
     if cfg.tie_word_embeddings or "lm_head.weight" not in index:
         lm_head = embed
     else:
         lm_head = get("lm_head.weight")[tp.rank * vs:(tp.rank + 1) * vs].to(device=device, dtype=dtype).contiguous()
-    return cfg, LlamaWeights(embed, layers, norm, lm_head, vocab_start=tp.rank * vs)
+    norm, lm_head = _final(norm, lm_head, fold_norms)
+    return cfg, LlamaWeights(embed, layers, norm, lm_head, vocab_start=tp.rank * vs, norms_folded=fold_norms)
 
 
 def load_meta(path: str, tp: TPContext | None = None, device="cpu", dtype=torch.bfloat16,
-              weight_dtype: str = "bf16") -> tuple[LlamaConfig, LlamaWeights]:
+              weight_dtype: str = "bf16", fold_norms: bool = True) -> tuple[LlamaConfig, LlamaWeights]:
     """Meta layout: params.json + consolidated.NN.pth (model-parallel shards are concatenated back first).
     Loaded with ``weights_only=True`` (no pickled code is ever executed)."""
     tp = tp or TPContext.single()
@@ -375,17 +408,19 @@ def load_meta(path: str, tp: TPContext | None = None, device="cpu", dtype=torch.
             gate=cat(p + "feed_forward.w1.weight", 0), up=cat(p + "feed_forward.w3.weight", 0),
             down=cat(p + "feed_forward.w2.weight", 1),
         )
-        layers.append(assemble_layer(cfg, tp, full, device, dtype, weight_dtype))
+        layers.append(assemble_layer(cfg, tp, full, device, dtype, weight_dtype, fold_norms))
     norm = cat("norm.weight", 0).to(device=device, dtype=dtype)
     lm_head = cat("output.weight", 0)[tp.rank * vs:(tp.rank + 1) * vs].to(device=device, dtype=dtype).contiguous()
-    return cfg, LlamaWeights(embed, layers, norm, lm_head, vocab_start=tp.rank * vs)
+    norm, lm_head = _final(norm, lm_head, fold_norms)
+    return cfg, LlamaWeights(embed, layers, norm, lm_head, vocab_start=tp.rank * vs, norms_folded=fold_norms)
 
 
-def load_checkpoint(path: str, tp: TPContext | None = None, device="cpu", weight_dtype: str = "bf16"):
+def load_checkpoint(path: str, tp: TPContext | None = None, device="cpu", weight_dtype: str = "bf16",
+                    fold_norms: bool = True):
     if os.path.exists(os.path.join(path, "config.json")):
-        return load_hf(path, tp, device, weight_dtype=weight_dtype)
+        return load_hf(path, tp, device, weight_dtype=weight_dtype, fold_norms=fold_norms)
     if os.path.exists(os.path.join(path, "params.json")):
-        return load_meta(path, tp, device, weight_dtype=weight_dtype)
+        return load_meta(path, tp, device, weight_dtype=weight_dtype, fold_norms=fold_norms)
     raise FileNotFoundError(f"{path}: neither an HF (config.json) nor a Meta (params.json) Llama checkpoint")
 
 
@@ -511,31 +546,52 @@ class LlamaModel:
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
 
     # ---- one micro-batch's pieces of a layer (bf16: x is a tensor; W8A8: x is (e4m3 bytes, row scales)) ----------
-    def _norm(self, h: torch.Tensor, resid: torch.Tensor | None, w: torch.Tensor):
-        """(resid <- h + resid) and the normalised projection input."""
+    def _norm(self, h, st: dict, w: torch.Tensor, first: bool = False):
+        """(st["resid"] <- h + st["resid"]) and the normalised projection input (first: the residual stream starts as
+        h itself).  When h is an ops.ResidOut (a decode producer already added the residual and summed the squares)
+        the result is an ops.LazyNorm that the consuming GEMV folds into its prologue: no norm launch."""
         eps = self.cfg.rms_eps
+        if isinstance(h, ops.ResidOut):
+            st["resid"] = h.s
+            return ops.LazyNorm(h.s, h.part, w, eps)
+        resid = None if first else st["resid"]
         if self.w.fp8:
             return ops.quant_rows(h, resid, w, eps, 1 if resid is None else 2)
         return ops.rmsnorm(h, w, eps) if resid is None else ops.add_rmsnorm(h, resid, w, eps)
 
+    def _out_proj(self, x: torch.Tensor, w: torch.Tensor, st: dict):
+        """Row-parallel output projection (o_proj / down_proj).  TP=1 decode (T <= 2): the GEMV that also adds the
+        residual and emits the next RMSNorm's partial sums (ops.ResidOut) — the norm then costs no launch."""
+        T = st["T"]
+        if (_FUSE_NORM and self.w.norms_folded and self.tp.world == 1 and x.is_cuda and st["sb"].tiles is None
+                and ops.resid_ok(T, w.shape[0], w.shape[1])):
+            return ops.gemv_resid(x, w, st["resid"])
+        return ops.linear(x, w)
+
     def _attn(self, li: int, lw: LayerWeights, st: dict, kv: KVCache) -> torch.Tensor:
         """Attention block up to the row-parallel o_proj; returns this rank's partial sum."""
         sb, T, x = st["sb"], st["T"], st["x"]
-        qkv = ops.qlinear(*x, lw.wqkv.q, lw.wqkv.s) if self.w.fp8 else ops.linear(x, lw.wqkv)
-        ops.rope_kv_write(qkv, sb.pos, sb.tok_seq, sb.block_table, self.cos_sin, st["q_buf"], kv.k[li], kv.v[li],
-                          self.hq, self.hkv, True, kv.k_scale[li], kv.v_scale[li])
+        if (not self.w.fp8 and _FUSE_NORM and ops.qkv_rope(
+                x, lw.wqkv, sb.pos, sb.tok_seq, sb.block_table, self.cos_sin, st["q_buf"], kv.k[li], kv.v[li],
+                self.hq, self.hkv, kv.k_scale[li], kv.v_scale[li])):
+            pass  # decode: QKV GEMV (+ folded norm) + RoPE / paged-KV write in one launch
+        else:
+            x = ops.LazyNorm.force(x)
+            qkv = ops.qlinear(*x, lw.wqkv.q, lw.wqkv.s) if self.w.fp8 else ops.linear(x, lw.wqkv)
+            ops.rope_kv_write(qkv, sb.pos, sb.tok_seq, sb.block_table, self.cos_sin, st["q_buf"], kv.k[li], kv.v[li],
+                              self.hq, self.hkv, True, kv.k_scale[li], kv.v_scale[li])
         attn = ops.paged_attention(st["q_buf"], kv.k[li], kv.v[li], sb.block_table, sb.q_start, sb.ctx_len, sb.tiles,
                                    sb.ntiles, sb.nqt, sb.nsplit, self.scale, kv.k_scale[li], kv.v_scale[li])
         if self.w.fp8:
             return ops.qlinear(*ops.quant_rows(attn.view(T, -1)), lw.wo.q, lw.wo.s)
-        return ops.linear(attn.view(T, -1), lw.wo)
+        return self._out_proj(attn.view(T, -1), lw.wo, st)
 
     def _mlp(self, lw: LayerWeights, st: dict) -> torch.Tensor:
         """SwiGLU MLP up to the row-parallel down_proj; returns this rank's partial sum."""
         x = st["x"]
         if self.w.fp8:
             return ops.qlinear(*ops.qgate_up_quant(*x, lw.w_gu.q, lw.w_gu.s), lw.w_down.q, lw.w_down.s)
-        return ops.linear(ops.gate_up_silu(x, lw.w_gu), lw.w_down)
+        return self._out_proj(ops.gate_up_silu(x, lw.w_gu), lw.w_down, st)
 
     def forward(self, sb: StepBatch, kv: KVCache, logits_dtype=torch.bfloat16) -> torch.Tensor:
         """Returns logits [B, V] for the token at sb.last_idx of every sequence (full vocab on every TP rank).
@@ -554,8 +610,9 @@ class LlamaModel:
         for p in parts:
             h = tp.all_reduce(ops.embedding(p.ids, w.embed, w.vocab_start))
             T = p.ids.numel()
-            states.append(dict(sb=p, T=T, resid=h, x=self._norm(h, None, w.layers[0].attn_norm),
-                               q_buf=torch.empty(T, self.hq, cfg.head_dim, device=h.device, dtype=h.dtype)))
+            st = dict(sb=p, T=T, resid=h, q_buf=torch.empty(T, self.hq, cfg.head_dim, device=h.device, dtype=h.dtype))
+            st["x"] = self._norm(h, st, w.layers[0].attn_norm, first=True)
+            states.append(st)
         L = len(w.layers)
         for li, lw in enumerate(w.layers):
             pend = [ar(self._attn(li, lw, st, kv)) for st in states]
@@ -563,18 +620,20 @@ class LlamaModel:
             for st, (o, work) in zip(states, pend):
                 if work is not None:
                     work.wait()
-                st["x"] = self._norm(o, st["resid"], lw.mlp_norm)
+                st["x"] = self._norm(o, st, lw.mlp_norm)
                 pend2.append(ar(self._mlp(lw, st)))
             for st, (dn, work) in zip(states, pend2):
                 if work is not None:
                     work.wait()
                 if li + 1 < L:
-                    st["x"] = self._norm(dn, st["resid"], w.layers[li + 1].attn_norm)
+                    st["x"] = self._norm(dn, st, w.layers[li + 1].attn_norm)
+                elif isinstance(dn, ops.ResidOut) and st["sb"].tiles is None:  # decode: every token is sampled
+                    st["x"] = self._norm(dn, st, w.norm)
                 else:  # only the sampled rows need the final norm + LM head (bf16)
                     li_ = st["sb"].last_idx
                     st["x"] = ops.add_rmsnorm(dn.index_select(0, li_), st["resid"].index_select(0, li_), w.norm,
                                               cfg.rms_eps)
-        x = states[0]["x"] if len(states) == 1 else torch.cat([st["x"] for st in states])
+        x = states[0]["x"] if len(states) == 1 else torch.cat([ops.LazyNorm.force(st["x"]) for st in states])
         logits = ops.linear(x, w.lm_head)
         logits = tp.all_gather_last(logits)
         return logits if logits.dtype == logits_dtype else logits.to(logits_dtype)

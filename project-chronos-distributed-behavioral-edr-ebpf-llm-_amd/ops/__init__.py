@@ -14,7 +14,7 @@ import os
 import torch
 
 from . import reference as ref
-from .gemm import gate_up_silu, linear  # noqa: F401  (re-export)
+from .gemm import LazyNorm, ResidOut, gate_up_silu, gemv_ok, gemv_resid, linear, resid_ok  # noqa: F401  (re-export)
 
 _loaded = False
 
@@ -117,6 +117,32 @@ def rope_kv_write(qkv, pos, tok_seq, block_table, cos_sin, q_out, k_cache, v_cac
     else:
         ref.rope_kv_write(qkv, pos, tok_seq, block_table, cos_sin, q_out, k_cache, v_cache, hq, hkv, write_q,
                           k_scale, v_scale)
+
+
+def qkv_rope(x, w_qkv, pos, tok_seq, block_table, cos_sin, q_out, k_cache, v_cache, hq: int, hkv: int,
+             k_scale: float = 1.0, v_scale: float = 1.0) -> bool:
+    """Decode QKV projection + RoPE + paged-KV write in one GEMV launch (csrc/kernels/gemv.hip ROPE epilogue), with the
+    input RMSNorm folded in when x is a LazyNorm.  Returns False (nothing done) off the decode GEMV shapes; the caller
+    then runs the unfused ops."""
+    lazy = isinstance(x, LazyNorm)
+    if lazy and not x.fusable():
+        return False
+    t = x.s if lazy else x
+    m, n, k = t.numel() // t.shape[-1], w_qkv.shape[0], t.shape[-1]
+    if not (t.is_cuda and m <= 2 and gemv_ok(m, n, k)):
+        return False
+    _k().qkv_rope(t.reshape(m, k), x.part if lazy else None, x.eps if lazy else 0.0, w_qkv,
+                  pos, tok_seq, block_table, cos_sin, q_out, k_cache, v_cache, hq, hkv, k_scale, v_scale)
+    return True
+
+
+def set_decode_gate(state: torch.Tensor | None, n: int = 0) -> None:
+    """Arm (1 <= n <= 8) / disarm (n = 0) the decode early-exit gate for the launches that follow: every kernel of a
+    decode step returns at once when none of ``state[:n]`` is live (chronos_hip.h).  No-op without the GPU library."""
+    if state is not None and state.is_cuda:
+        _k().set_decode_gate(state, n)
+    elif _loaded:
+        torch.ops.chronos.set_decode_gate(None, 0)
 
 
 def paged_attention(q, k_cache, v_cache, block_table, q_start, ctx_len, tiles=None, ntiles: int = 0, nqt: int = 1,

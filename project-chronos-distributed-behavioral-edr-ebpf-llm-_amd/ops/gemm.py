@@ -13,6 +13,7 @@ Routing is by measured shape (profiles/r1_gemm_vs_hipblaslt.json, cold weights, 
 """
 from __future__ import annotations
 
+from dataclasses import dataclass
 from typing import Callable, Optional
 
 import torch
@@ -23,6 +24,65 @@ _custom: list[tuple[Callable[[int, int, int], bool], Callable[[torch.Tensor, tor
 
 def register(pred: Callable[[int, int, int], bool], fn: Callable[[torch.Tensor, torch.Tensor], torch.Tensor]) -> None:
     _custom.append((pred, fn))
+
+
+@dataclass
+class ResidOut:
+    """Output of a decode producer GEMV with the residual epilogue (``gemv_resid``): the new residual stream
+    ``s = bf16(bf16(x @ w.T) + resid)`` and the per-workgroup partial sums of s^2 the next RMSNorm needs."""
+    s: torch.Tensor
+    part: torch.Tensor
+
+
+@dataclass
+class LazyNorm:
+    """``rmsnorm(s) * w`` of a residual stream a ResidOut producer just wrote, not computed yet.
+
+    Only built for models whose norm weights are folded into the consuming projections (``w`` is then ones).  A decode
+    GEMV consumer (``linear`` / ``gate_up_silu`` / the fused QKV projection) applies it as one per-row scale of its
+    outputs (csrc/kernels/gemv.hip NORMP: inv from the producer's partials), so the norm costs no launch; any other
+    consumer calls ``materialize`` (the standalone RMSNorm kernel: equal up to rounding)."""
+    s: torch.Tensor
+    part: torch.Tensor
+    w: torch.Tensor
+    eps: float
+    _y: Optional[torch.Tensor] = None
+
+    @property
+    def shape(self):
+        return self.s.shape
+
+    def rows(self) -> int:
+        return self.s.numel() // self.s.shape[-1]
+
+    def fusable(self) -> bool:
+        return self.s.is_cuda and self._y is None
+
+    def materialize(self) -> torch.Tensor:
+        if self._y is None:
+            from . import rmsnorm
+
+            self._y = rmsnorm(self.s, self.w, self.eps)
+        return self._y
+
+    @staticmethod
+    def force(x):
+        """A tensor for anything that is not a GEMV consumer."""
+        return x.materialize() if isinstance(x, LazyNorm) else x
+
+
+def gemv_resid(x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor) -> ResidOut:
+    """Decode producer: the new residual stream and the RMSNorm partials in one GEMV launch (M <= 2)."""
+    from . import _k
+
+    s = torch.empty(resid.shape, dtype=resid.dtype, device=resid.device)
+    part = _k().gemv_resid(x.reshape(-1, x.shape[-1]), w, resid, s)
+    return ResidOut(s, part)
+
+
+def resid_ok(m: int, n: int, k: int) -> bool:
+    """Shapes of the residual-epilogue producer (gemv.hip kResid): the M <= 2 GEMV shapes."""
+    return m <= 2 and gemv_ok(m, n, k)
 
 
 def gemv_ok(m: int, n: int, k: int, swiglu: bool = False) -> bool:
@@ -56,8 +116,13 @@ def mfma_gemm(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False, stages: in
 
 def gate_up_silu(x: torch.Tensor, w_gu: torch.Tensor) -> torch.Tensor:
     """silu(x @ gate.T) * (x @ up.T) with w_gu = [gate; up]: one fused launch for decode batches, else GEMM + silu_mul."""
-    from . import silu_mul
+    from . import _k, silu_mul
 
+    if isinstance(x, LazyNorm):
+        m, n, k = x.rows(), w_gu.shape[0], x.shape[-1]
+        if x.fusable() and gemv_ok(m, n, k, swiglu=True):
+            return _k().gemv_normp(x.s, x.part, x.eps, w_gu, True)
+        x = x.materialize()
     if x.is_cuda:
         m, n, k = x.numel() // x.shape[-1], w_gu.shape[0], x.shape[-1]
         if gemv_ok(m, n, k, swiglu=True):
@@ -67,7 +132,13 @@ def gate_up_silu(x: torch.Tensor, w_gu: torch.Tensor) -> torch.Tensor:
     return silu_mul(linear(x, w_gu))
 
 
-def linear(x: torch.Tensor, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+def linear(x, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if isinstance(x, LazyNorm):
+        if x.fusable() and out is None and gemv_ok(x.rows(), w.shape[0], x.shape[-1]):
+            from . import _k
+
+            return _k().gemv_normp(x.s, x.part, x.eps, w, False)
+        x = x.materialize()
     if x.is_cuda:
         m, k = x.numel() // x.shape[-1], x.shape[-1]
         n = w.shape[0]

@@ -1,0 +1,83 @@
+"""Single-sensor-stream verdict latency (BASELINE config "Llama-3 8B bf16 TP=1 on one MI355X, single sensor stream").
+
+One chain in flight at a time, exactly like the reference's blocking analyze_sequence (chronos_sensor.py:117-119):
+prefill the kill-chain prompt, decode the schema-constrained verdict, parse it.  Prints p50/p90 latency and the mean
+per-token decode time; ``--ab`` runs the fused decode path (norm-in-GEMV, fused QKV+RoPE, decode gate) and the unfused
+one on two engines in ONE process, interleaved (cdna_hip_programming.md §5.4 rule 24).
+
+  python scripts/single_stream.py --chains 16 [--ab] [--out gpurun_out/single.json]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+# name -> (fused decode kernels, decode early-exit gate)
+VARIANTS = {"fused": (True, True), "fused_nogate": (True, False), "unfused_gate": (False, True),
+            "unfused": (False, False)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--chains", type=int, default=16)
+    ap.add_argument("--num-predict", type=int, default=64)
+    ap.add_argument("--burst", type=int, default=8)
+    ap.add_argument("--ab", action="store_true")
+    ap.add_argument("--only", choices=list(VARIANTS), default="fused", help="variant without --ab")
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+
+    import torch
+
+    from chronos.brain.engine.engine import Engine, EngineConfig
+    from chronos.models import llama
+    from chronos.sensor.prompt import VERDICT_SCHEMA, build_prompt
+    from chronos.sensor.replay import synthetic_chains
+
+    prompts = [build_prompt(c.history) for c in synthetic_chains(a.chains + 1, seed=7)]
+    variants = list(VARIANTS) if a.ab else [a.only]
+    engines = {}
+    for name in variants:
+        fuse, gate = VARIANTS[name]
+        llama._FUSE_NORM = fuse
+        eng = Engine(EngineConfig(model=a.model, device="cuda", max_slots=8, max_model_len=512, decode_burst=a.burst,
+                                  decode_gate=gate, seed=0))
+        # capture the n=1 graph under this variant's setting
+        eng.submit(prompts[0], fmt=VERDICT_SCHEMA, num_predict=a.num_predict)
+        eng.run_until_idle()
+        engines[name] = (eng, fuse)
+    res = {name: [] for name in variants}
+    for p in prompts[1:]:
+        for name, (eng, fuse) in engines.items():
+            llama._FUSE_NORM = fuse
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            r = eng.submit(p, fmt=VERDICT_SCHEMA, num_predict=a.num_predict)
+            eng.run_until_idle()
+            dt = time.perf_counter() - t0
+            json.loads(r.text)
+            res[name].append((dt, len(r.out_ids), r.t_first - r.t_submit))
+    out = {}
+    for name, rows in res.items():
+        lat = [x[0] for x in rows]
+        toks = [x[1] for x in rows]
+        ttft = [x[2] for x in rows]
+        out[name] = dict(p50_ms=round(1e3 * statistics.median(lat), 2),
+                         p90_ms=round(1e3 * sorted(lat)[int(0.9 * (len(lat) - 1))], 2),
+                         mean_tokens=round(statistics.mean(toks), 1),
+                         ttft_p50_ms=round(1e3 * statistics.median(ttft), 2),
+                         ms_per_token=round(1e3 * sum(x[0] - x[2] for x in rows) / max(1, sum(toks)), 3))
+    print(json.dumps(out))
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

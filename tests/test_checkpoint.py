@@ -122,3 +122,20 @@ def test_tp_sharded_load_is_a_partition(tmp_path):
         assert torch.equal(down, f.w_down)
     emb = torch.cat([s.embed for s in shards])
     assert torch.equal(emb, full.embed) and shards[1].vocab_start == cfg.vocab_size // 2
+
+
+def test_folded_norms_match_unfolded(tmp_path):
+    """RMSNorm weights folded into QKV / gate_up / LM head (the decode GEMV's fused-norm layout) give the same logits
+    as the unfolded model, to bf16 rounding of W diag(w); the folded model stores its norms as ones."""
+    cfg = get_config("tiny")
+    t = _hf_tensors(cfg, seed=5)
+    t["model.norm.weight"] = (1 + torch.rand(cfg.hidden_size) * 0.2).to(torch.bfloat16)
+    _write_hf(str(tmp_path / "hf"), cfg, t)
+    c1, wf = load_checkpoint(str(tmp_path / "hf"))
+    c2, wu = load_checkpoint(str(tmp_path / "hf"), fold_norms=False)
+    assert wf.norms_folded and not wu.norms_folded
+    assert bool((wf.layers[0].attn_norm == 1).all()) and bool((wf.norm == 1).all())
+    assert not bool((wu.layers[0].attn_norm == 1).all())
+    lf, lu = _logits(c1, wf), _logits(c2, wu)
+    assert (lf - lu).abs().max() <= 0.02 * lu.abs().max() + 1e-3
+    assert (lf.argmax(-1) == lu.argmax(-1)).float().mean() >= 0.9

@@ -1,0 +1,204 @@
+"""Fused decode-step kernels (csrc/kernels/gemv.hip NORM / ROPE variants) and the decode early-exit gate.
+
+Each fused op is checked against the unfused kernel chain it replaces (standalone RMSNorm -> GEMV, GEMV -> RoPE +
+paged-KV write): same bits where the arithmetic order is the same, fp32-reference tolerance otherwise.  The gate test
+arms it on an all-finished state vector and checks that every gated kernel leaves its outputs untouched.
+"""
+import json
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    from chronos import ops
+
+    ops.load()
+    import chronos.native as n
+
+    assert "_C" in n._loaded, "HIP kernel library must be the one running"
+
+
+def _rand(g, *shape, scale=1.0):
+    return (torch.randn(*shape, device=DEV, generator=g) * scale).to(torch.bfloat16)
+
+
+def _close(a, b, atol, rtol):
+    d = (a.float() - b.float()).abs()
+    assert bool((d <= atol + rtol * b.float().abs()).all()), f"max err {float(d.max()):.4g}"
+
+
+@pytest.mark.parametrize("m", [1, 2])
+@pytest.mark.parametrize("n_out", [4096, 8192])
+def test_gemv_resid_producer(m, n_out):
+    """resid_out = bf16(bf16(x W^T) + resid) bit-exact vs GEMV + add; partials sum to sum(resid_out^2)."""
+    from chronos import ops
+    from chronos.ops import gemm
+
+    g = torch.Generator(device=DEV).manual_seed(m + n_out)
+    x = _rand(g, m, 4096)
+    w = _rand(g, n_out, 4096, scale=0.02)
+    r = _rand(g, m, n_out)
+    out = ops.gemv_resid(x, w, r)
+    exp = (gemm._gemv(x, w).float() + r.float()).to(torch.bfloat16)
+    assert torch.equal(out.s, exp)
+    assert out.part.shape == (m, n_out // 8)
+    ss = exp.float().pow(2).sum(-1)
+    _close(out.part.sum(-1), ss, 1e-3, 1e-5)
+
+
+@pytest.mark.parametrize("m", [1, 2])
+@pytest.mark.parametrize("swiglu,n", [(False, 6144), (True, 2 * 1792)])
+def test_gemv_normp_consumer(m, swiglu, n):
+    """The folded norm (norm weight inside W, inv from the producer's partials) equals the standalone RMSNorm -> GEMV
+    on the unfolded weights, to bf16 rounding; and it is deterministic."""
+    from chronos import ops
+    from chronos.models.llama import fold_norm
+    from chronos.ops import gemm
+
+    g = torch.Generator(device=DEV).manual_seed(m * 3 + n)
+    x = _rand(g, m, 4096)
+    wo = _rand(g, 4096, 4096, scale=0.02)
+    r = _rand(g, m, 4096, scale=2.0)
+    nw = (torch.rand(4096, device=DEV, generator=g) + 0.5).to(torch.bfloat16)
+    w = _rand(g, n, 4096, scale=0.02)
+    wf = fold_norm(w, nw)
+    ones = torch.ones_like(nw)
+    prod = ops.gemv_resid(x, wo, r)
+    ln = ops.LazyNorm(prod.s, prod.part, ones, 1e-5)
+    y = ops.gate_up_silu(ln, wf) if swiglu else ops.linear(ln, wf)
+    y_ref = gemm._gemv(ops.rmsnorm(prod.s, nw, 1e-5), w, swiglu)
+    _close(y, y_ref, 2.5e-2, 2.5e-2)  # |err| ~ 2^-9 * std(y) per rounding (W diag(w) and s * inv), absolute
+    ln2 = ops.LazyNorm(prod.s, prod.part, ones, 1e-5)
+    y2 = ops.gate_up_silu(ln2, wf) if swiglu else ops.linear(ln2, wf)
+    assert torch.equal(y, y2)
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+@pytest.mark.parametrize("m,hq,hkv", [(1, 32, 8), (2, 32, 8), (1, 8, 1)])
+@pytest.mark.parametrize("folded", [False, True])
+def test_qkv_rope_equals_unfused(fp8, m, hq, hkv, folded):
+    """QKV GEMV + RoPE/paged-KV epilogue == GEMV then rope_kv_write (bit-exact on a plain input; with the folded norm
+    — norm weight inside W, inv from partials — against the standalone-norm chain, to bf16 rounding)."""
+    from chronos import ops
+    from chronos.models.llama import get_config, rope_table
+    from chronos.ops import gemm
+
+    g = torch.Generator(device=DEV).manual_seed(hq + m + fp8 + 10 * folded)
+    k, bs, nb = 4096, 16, 40
+    s = _rand(g, m, k, scale=2.0)
+    w = _rand(g, (hq + 2 * hkv) * 128, k, scale=0.02)
+    nw = (torch.rand(k, device=DEV, generator=g) + 0.5).to(torch.bfloat16)
+    cs = rope_table(get_config("llama3.1-8b"), 2048, DEV)
+    bt = torch.randperm(nb, device=DEV, generator=g).to(torch.int32).view(2, nb // 2)
+    pos = torch.tensor([333, 17][:m], dtype=torch.int32, device=DEV)
+    tok_seq = torch.arange(m, dtype=torch.int32, device=DEV)
+    if fp8:
+        kc = torch.randint(0, 100, (nb, hkv, bs, 128), dtype=torch.uint8, device=DEV)
+        vc = torch.randint(0, 100, (nb, hkv, 128, bs), dtype=torch.uint8, device=DEV)
+        ks, vs = 0.5, 0.25
+    else:
+        kc = _rand(g, nb, hkv, bs, 128)
+        vc = _rand(g, nb, hkv, 128, bs)
+        ks = vs = 1.0
+    kc2, vc2 = kc.clone(), vc.clone()
+    q1 = torch.zeros(m, hq, 128, device=DEV, dtype=torch.bfloat16)
+    q2 = torch.zeros_like(q1)
+    x = ops.rmsnorm(s, nw, 1e-5)
+    ops.rope_kv_write(gemm._gemv(x, w), pos, tok_seq, bt, cs, q2, kc2, vc2, hq, hkv, True, ks, vs)
+    if folded:
+        from chronos.models.llama import fold_norm
+
+        part = s.float().pow(2).view(m, -1, 8).sum(-1).contiguous()  # a producer's partials for s
+        src, wq = ops.LazyNorm(s, part, torch.ones_like(nw), 1e-5), fold_norm(w, nw)
+    else:
+        src, wq = x, w
+    assert ops.qkv_rope(src, wq, pos, tok_seq, bt, cs, q1, kc, vc, hq, hkv, ks, vs)
+    torch.cuda.synchronize()
+    if folded:
+        _close(q1, q2, 2e-2, 2e-2)
+        if fp8:  # dequantised e4m3: one rounding step (2^-3 relative) or a near-zero sign flip apart
+            f8 = lambda t: t.view(torch.float8_e4m3fn).float()  # noqa: E731
+            _close(f8(kc), f8(kc2), 4e-2 / ks, 0.13)
+            _close(f8(vc), f8(vc2), 4e-2 / vs, 0.13)
+        else:
+            _close(kc, kc2, 2e-2, 2e-2)
+            _close(vc, vc2, 2e-2, 2e-2)
+    else:
+        assert torch.equal(q1, q2)
+        assert torch.equal(kc, kc2)
+        assert torch.equal(vc, vc2)
+
+
+def test_decode_gate_skips_finished_steps():
+    """Armed on a state vector with no live row, in-place kernels (residual norm, fused QKV + KV write) leave their
+    outputs untouched; one live row and they run again."""
+    from chronos import ops
+    from chronos.models.llama import get_config, rope_table
+
+    g = torch.Generator(device=DEV).manual_seed(3)
+    hq, hkv, k = 8, 1, 4096
+    x = _rand(g, 1, k)
+    r = _rand(g, 1, k)
+    nw = (torch.rand(k, device=DEV, generator=g) + 0.5).to(torch.bfloat16)
+    w = _rand(g, (hq + 2 * hkv) * 128, k, scale=0.02)
+    cs = rope_table(get_config("llama3-8b"), 64, DEV)
+    bt = torch.arange(4, dtype=torch.int32, device=DEV).view(1, 4)
+    pos = torch.tensor([5], dtype=torch.int32, device=DEV)
+    ts = torch.zeros(1, dtype=torch.int32, device=DEV)
+    kc, vc = _rand(g, 4, hkv, 16, 128), _rand(g, 4, hkv, 128, 16)
+    q = torch.zeros(1, hq, 128, device=DEV, dtype=torch.bfloat16)
+    r0, kc0, vc0 = r.clone(), kc.clone(), vc.clone()
+    state = torch.tensor([0, -1, 0, 0], dtype=torch.int32, device=DEV)  # DONE / empty: nothing live
+
+    def run():
+        ops.add_rmsnorm(x, r, nw, 1e-5)
+        assert ops.qkv_rope(x, w, pos, ts, bt, cs, q, kc, vc, hq, hkv)
+
+    try:
+        ops.set_decode_gate(state, 4)
+        run()
+        torch.cuda.synchronize()
+        assert torch.equal(r, r0) and torch.equal(kc, kc0) and torch.equal(vc, vc0)
+        assert not bool(q.abs().sum())
+        state[2] = 5  # one live row: the same launches compute again
+        run()
+        torch.cuda.synchronize()
+    finally:
+        ops.set_decode_gate(None, 0)
+    assert not torch.equal(r, r0) and not torch.equal(kc, kc0) and not torch.equal(vc, vc0)
+    assert bool(q.abs().sum())
+
+
+def test_engine_fused_decode_matches_unfused(monkeypatch):
+    """Greedy verdicts with the fused decode path + gate vs the separate kernels (one stream and two, graphs on): the
+    folded norm sums squares in another order, so the first tokens must agree and the verdicts must parse; the fused
+    engine is deterministic run to run."""
+    from chronos.brain.engine.engine import Engine, EngineConfig
+    from chronos.models import llama
+    from chronos.sensor.prompt import VERDICT_SCHEMA, build_prompt
+
+    chains = [["[OPEN] attack_chain.sh -> /tmp/malware.bin", "[EXEC] attack_chain.sh -> curl"],
+              ["[EXEC] bash -> chmod", "[OPEN] chmod -> /tmp/x", "[EXEC] bash -> cat"]]
+    outs = []
+    for fuse in (True, False, True):
+        monkeypatch.setattr(llama, "_FUSE_NORM", fuse)
+        res = []
+        for n in (1, 2):
+            eng = Engine(EngineConfig(model="small", device=DEV, max_slots=n, max_model_len=256, decode_burst=8,
+                                      decode_gate=fuse))
+            reqs = [eng.submit(build_prompt(c), fmt=VERDICT_SCHEMA, num_predict=40) for c in chains[:n]]
+            eng.run_until_idle()
+            for r in reqs:
+                json.loads(r.text)
+            res.append([r.out_ids for r in reqs])
+        outs.append(res)
+    assert outs[0] == outs[2]
+    for a, b in zip(outs[0], outs[1]):
+        for x, y in zip(a, b):
+            assert x[:8] == y[:8]
