@@ -20,6 +20,7 @@ Work per GPU is fixed as N grows (weak scaling).  Rank 0 prints ONE JSON line.
 from __future__ import annotations
 
 import argparse
+import collections
 import json
 import math
 import os
@@ -168,6 +169,8 @@ def main():
             pass
     lat = [r.latency for r in timed]
     gen_tok = sum(len(r.out_ids) for r in timed)
+    hist = collections.Counter(min(len(r.out_ids) // 4 * 4, 64) for r in timed)
+    progress("verdict length histogram (4-token bins): " + json.dumps(dict(sorted(hist.items()))))
     prompt_tok = sum(len(r.prompt_ids) for r in timed)
 
     # single-stream latency (the reference's regime: one chain in flight)
