@@ -51,6 +51,10 @@ def parse():
     ap.add_argument("--weights", choices=["bf16", "fp8"], default="bf16",
                     help="fp8 = W8A8 e4m3 projections on the block-scaled MFMA / hipBLASLt fp8 (not the headline)")
     ap.add_argument("--device", default="cuda")
+    ap.add_argument("--tp", type=int, default=1,
+                    help="tensor-parallel degree per replica (e.g. --model llama3-70b --tp 8): the world is split into "
+                         "world/tp replicas, each a lockstep TP engine over RCCL (+ the IPC one-shot all-reduce)")
+    ap.add_argument("--max-model-len", type=int, default=512)
     return ap.parse_args()
 
 
@@ -106,19 +110,32 @@ def main():
     if world > 1:
         dist.init_process_group("nccl" if cuda else "gloo")
     device = torch.device(f"cuda:{local}" if cuda else "cpu")
+    if world % a.tp:
+        raise SystemExit(f"--tp {a.tp} must divide the world size {world}")
+    replica, tp_rank = rank // a.tp, rank % a.tp
 
     from chronos.brain.engine.engine import Engine, EngineConfig
+    from chronos.parallel.tp import TPContext
     from chronos.sensor.prompt import VERDICT_SCHEMA, build_prompt
     from chronos.sensor.replay import synthetic_chains
 
-    cfg = EngineConfig(model=a.model, device=str(device), max_slots=a.streams, max_model_len=512,
+    tp = TPContext.single()
+    if a.tp > 1:
+        # every rank creates every replica's group (new_group is collective), keeps its own
+        groups = [dist.new_group(list(range(r * a.tp, (r + 1) * a.tp))) for r in range(world // a.tp)]
+        tp = TPContext(tp_rank, a.tp, groups[replica])
+        if cuda:
+            tp.enable_ipc_allreduce()
+    cfg = EngineConfig(model=a.model, device=str(device), max_slots=a.streams, max_model_len=a.max_model_len,
                        default_num_predict=a.num_predict, decode_burst=a.burst, use_graphs=not a.no_graphs,
                        prefix_cache=not a.no_prefix_cache, async_harvest=a.async_harvest, seed=0,
                        weight_dtype=a.weights)
-    eng = Engine(cfg)
+    # TP: the ranks of a replica submit the same chains in the same order and step the same deterministic scheduler,
+    # so they stay in lockstep by construction (the serving path adds the leader broadcast of parallel/tp_engine.py)
+    eng = Engine(cfg, tp=tp)
     total_steps = a.warmup + a.steps
     per_stream = total_steps if a.mode == "wave" else 2 * total_steps + 2  # closed loop: fast streams cycle more
-    chains = synthetic_chains(a.streams * per_stream + a.single_stream, seed=1000 + rank)
+    chains = synthetic_chains(a.streams * per_stream + a.single_stream, seed=1000 + replica)
     prompts = [build_prompt(c.history) for c in chains]
 
     def run_step(batch):
@@ -180,7 +197,7 @@ def main():
     single_lat = [r.latency for r in single[1:]] or [r.latency for r in single]
 
     stats = dict(elapsed=elapsed, ok=ok, n=len(timed), lat=lat, gen=gen_tok, ptok=prompt_tok, single=single_lat,
-                 hits=hits)
+                 hits=hits, tp_rank=tp_rank)
     if world > 1:
         allst = [None] * world
         dist.all_gather_object(allst, stats)
@@ -188,13 +205,18 @@ def main():
         allst = [stats]
     if rank == 0:
         t = max(s["elapsed"] for s in allst)
+        allst = [s for s in allst if s["tp_rank"] == 0]  # one report per replica (its TP ranks served the same chains)
         n = sum(s["n"] for s in allst)
         oks = sum(s["ok"] for s in allst)
         lats = [x for s in allst for x in s["lat"]]
         singles = [x for s in allst for x in s["single"]]
         chains_s = n / t
+        nrep = len(allst)
+        metric = "syscall-chains/sec analyzed + p50 verdict latency, Llama-3-8B TP=1"
+        if a.tp > 1 or a.model != "llama3-8b":
+            metric = f"syscall-chains/sec analyzed + p50 verdict latency, {a.model} TP={a.tp}"
         out = {
-            "metric": "syscall-chains/sec analyzed + p50 verdict latency, Llama-3-8B TP=1",
+            "metric": metric,
             "value": round(chains_s, 3),
             "unit": "chains/s",
             "n_gpus": world,
@@ -207,9 +229,10 @@ def main():
             "dtype": "bf16" if a.weights == "bf16" else "fp8-e4m3 W8A8 projections (bf16 norms/attention/KV/LM head)",
             "data": "synthetic syscall-chain telemetry (reference prompt template), random-init weights",
             "config": {
-                "model": a.model, "global_batch": a.streams * world, "seq_len": 512,
-                "parallelism": f"dp{world}" if world > 1 else "tp1",
-                "streams_per_gpu": a.streams, "num_predict": a.num_predict,
+                "model": a.model, "global_batch": a.streams * nrep, "seq_len": a.max_model_len,
+                "parallelism": (f"tp{a.tp}" + (f"dp{nrep}" if nrep > 1 else "")) if a.tp > 1 else
+                               (f"dp{world}" if world > 1 else "tp1"),
+                "streams_per_gpu": a.streams // a.tp, "streams_per_replica": a.streams, "num_predict": a.num_predict,
                 "format": "verdict JSON schema (constrained decode)",
                 "mode": "wave: a step = one wave of --streams chains arriving together" if a.mode == "wave" else
                         "closed: --streams streams each keep one chain in flight; a step = --streams completions",

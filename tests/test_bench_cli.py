@@ -1,0 +1,46 @@
+"""bench.py under torch.distributed.run on the CPU (gloo): the driver's multi-rank contract (one JSON line from rank 0,
+whole-job aggregate) for DP replicas and for TP replicas (--tp 2: the 70B TP=8 serving shape, here at TP=2 on the
+tiny model), without GPUs."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(extra):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr=127.0.0.1", f"--master-port={_port()}", os.path.join(REPO, "bench.py"), "--gpus", "2",
+           "--device", "cpu", "--model", "tiny", "--streams", "3", "--steps", "1", "--warmup", "1",
+           "--num-predict", "24", "--single-stream", "2", "--no-graphs", "--max-model-len", "384"] + extra
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=env, cwd=REPO)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("tp", [1, 2])
+def test_bench_two_ranks(tp):
+    r = _run(["--tp", str(tp)] if tp > 1 else [])
+    assert r["n_gpus"] == 2 and r["steps"] == 1 and r["value"] > 0
+    if tp == 1:
+        assert r["config"]["parallelism"] == "dp2" and r["config"]["global_batch"] == 6
+        assert r["verdicts_valid"] == "6/6"
+    else:
+        assert r["config"]["parallelism"] == "tp2" and r["config"]["global_batch"] == 3
+        assert r["verdicts_valid"] == "3/3" and "TP=2" in r["metric"]
