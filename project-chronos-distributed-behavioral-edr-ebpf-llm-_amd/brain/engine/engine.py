@@ -75,6 +75,7 @@ class EngineConfig:
     tp_overlap: bool = True        # TP prefill: two micro-batches, each one's RCCL all-reduces overlap the other's compute
     tp_overlap_min_tokens: int = 1024
     decode_gate: bool = True       # small buckets: kernels of steps after the last live row finished return at once
+    cp_min_tokens: int = 4096      # context parallel (Engine(cp=...)): prefill chunks at least this long are split
 
 
 @dataclass
@@ -134,9 +135,16 @@ class _Snapshot:
 
 class Engine:
     def __init__(self, cfg: EngineConfig, tp: TPContext | None = None, model: LlamaModel | None = None,
-                 tokenizer=None):
+                 tokenizer=None, cp: TPContext | None = None):
+        """``cp``: a context-parallel group (full weights on every rank, parallel/context_parallel.py).  Its ranks
+        run this engine in lockstep (same submissions, same order); long prefill chunks are split across them and
+        each prefill step covers ``max_prefill_tokens`` per rank."""
         self.cfg = cfg
         self.tp = tp or TPContext.single()
+        self.cp = cp or TPContext.single()
+        if self.cp.world > 1 and self.tp.world > 1:
+            raise ValueError("context parallelism runs on full-weight (TP=1) ranks")
+        self._chunk = cfg.max_prefill_tokens * self.cp.world
         self.device = torch.device(cfg.device)
         if self.device.type == "cuda" and self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
@@ -164,12 +172,13 @@ class Engine:
                 nb = max(2, min(nb, need))
             else:
                 nb = need
-        if self.tp.world > 1:  # lockstep TP scheduling needs the same block budget on every rank
-            import torch.distributed as dist
+        for grp in (self.tp, self.cp):  # lockstep TP / CP scheduling needs the same block budget on every rank
+            if grp.world > 1:
+                import torch.distributed as dist
 
-            t = torch.tensor([nb], dtype=torch.int64, device=self.device)
-            dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.tp.group)
-            nb = int(t.item())
+                t = torch.tensor([nb], dtype=torch.int64, device=self.device)
+                dist.all_reduce(t, op=dist.ReduceOp.MIN, group=grp.group)
+                nb = int(t.item())
         self.kv = KVCache(mc, self.tp, nb, bs, self.device, cfg.kv_dtype, cfg.kv_scale, cfg.kv_scale)
         self.blocks = BlockManager(nb, bs, prefix_cache=cfg.prefix_cache)
         # ---- slot state (device) ----
@@ -365,7 +374,7 @@ class Engine:
     def _admit(self) -> None:
         slots, rows = [], []
         # admit about one prefill chunk ahead: the rest stays queued (and untokenized) while that chunk computes
-        budget = self.cfg.max_prefill_tokens - sum(len(r.prompt_ids) - r.prefilled for r in self.prefilling)
+        budget = self._chunk - sum(len(r.prompt_ids) - r.prefilled for r in self.prefilling)
         with self._lock:
             while self.waiting and self.free_slots and budget > 0:
                 req = self.waiting[0]
@@ -400,7 +409,7 @@ class Engine:
                 torch.tensor(rows, dtype=torch.int32), self.device)
 
     def _prefill_step(self) -> None:
-        budget = self.cfg.max_prefill_tokens
+        budget = self._chunk
         chunks, starts, bts, reqs = [], [], [], []
         for req in self.prefilling:
             if budget <= 0:
@@ -412,10 +421,21 @@ class Engine:
             reqs.append(req)
             budget -= n
         ntok = sum(len(c) for c in chunks)
-        split = 2 if (self.tp.world > 1 and self.cfg.tp_overlap and ntok >= self.cfg.tp_overlap_min_tokens) else 1
-        sb = make_prefill_batch(chunks, starts, bts, self.model.cfg, self.tp, self.device,
-                                max_blocks=self.max_blocks_per_seq, nqt=self.cfg.prefill_nqt, split=split)
-        logits = self.model.forward(sb, self.kv)
+        if (self.cp.world > 1 and len(chunks) == 1
+                and ntok >= max(self.cfg.cp_min_tokens, 2 * self.cp.world)):  # context-parallel chunk
+            from ...parallel.context_parallel import last_logits, make_cp_batch
+
+            sb = make_cp_batch(chunks[0], starts[0], bts[0], self.model.cfg, self.cp, self.device,
+                               self.max_blocks_per_seq, nqt=self.cfg.prefill_nqt)
+            logits = last_logits(self.model.forward(sb, self.kv), self.cp)
+            self.stats["cp_prefill_steps"] += 1
+        else:
+            chunks, starts, bts, reqs = self._fit(chunks, starts, bts, reqs)
+            ntok = sum(len(c) for c in chunks)
+            split = 2 if (self.tp.world > 1 and self.cfg.tp_overlap and ntok >= self.cfg.tp_overlap_min_tokens) else 1
+            sb = make_prefill_batch(chunks, starts, bts, self.model.cfg, self.tp, self.device,
+                                    max_blocks=self.max_blocks_per_seq, nqt=self.cfg.prefill_nqt, split=split)
+            logits = self.model.forward(sb, self.kv)
         done_rows, done_reqs = [], []
         for i, (req, ch) in enumerate(zip(reqs, chunks)):
             req.prefilled += len(ch)
@@ -423,7 +443,7 @@ class Engine:
                 done_rows.append(i)
                 done_reqs.append(req)
                 self.blocks.register(req.prompt_ids, req.blocks)
-        self.stats["prefill_tokens"] += int(sb.ids.numel())
+        self.stats["prefill_tokens"] += ntok
         self.stats["prefill_steps"] += 1
         if not done_reqs:
             return
@@ -453,6 +473,21 @@ class Engine:
             self.running[r.slot] = r
             if "cancel_reason" in r.meta:  # cancelled mid-prefill: its blocks are computed now, drop it next step
                 self.cancel(r, r.meta["cancel_reason"])
+
+    def _fit(self, chunks, starts, bts, reqs):
+        """A replicated (non-CP) prefill step covers at most max_prefill_tokens: with CP the admission budget is
+        W times that, so trim the packed chunks back to one rank's worth."""
+        if self._chunk == self.cfg.max_prefill_tokens:
+            return chunks, starts, bts, reqs
+        out, left = ([], [], [], []), self.cfg.max_prefill_tokens
+        for c, s0, bt, r in zip(chunks, starts, bts, reqs):
+            if left <= 0:
+                break
+            c = c[:left]
+            for lst, v in zip(out, (c, s0, bt, r)):
+                lst.append(v)
+            left -= len(c)
+        return out
 
     def _decode_rows(self) -> int:
         return _bucket(max(self.running) + 1) if self.running else 0

@@ -471,6 +471,9 @@ class StepBatch:
     # micro-batches over contiguous sequence ranges (TP prefill): the forward interleaves them layer by layer so the
     # RCCL all-reduce of one runs on its stream while the other computes (LlamaModel.forward)
     parts: Optional[list] = None
+    # context-parallel prefill (parallel/context_parallel.py): this rank holds part of a long chunk; K/V are
+    # all-gathered per layer and written for every token of the chunk
+    cp: Optional[object] = None
 
 
 def make_prefill_batch(prompts: list[list[int]], starts: list[int], block_tables: list[list[int]], cfg: LlamaConfig,
@@ -580,6 +583,12 @@ class LlamaModel:
             qkv = ops.qlinear(*x, lw.wqkv.q, lw.wqkv.s) if self.w.fp8 else ops.linear(x, lw.wqkv)
             ops.rope_kv_write(qkv, sb.pos, sb.tok_seq, sb.block_table, self.cos_sin, st["q_buf"], kv.k[li], kv.v[li],
                               self.hq, self.hkv, True, kv.k_scale[li], kv.v_scale[li])
+            if sb.cp is not None:  # CP: every rank writes the whole chunk's K/V before any rank attends
+                from ..parallel.context_parallel import gather_kv
+
+                cp = sb.cp
+                ops.rope_kv_write(gather_kv(qkv, self.hq, cp), cp.pos_all, cp.seq_all, cp.bt, self.cos_sin,
+                                  cp.dummy_q, kv.k[li], kv.v[li], 0, self.hkv, False, kv.k_scale[li], kv.v_scale[li])
         attn = ops.paged_attention(st["q_buf"], kv.k[li], kv.v[li], sb.block_table, sb.q_start, sb.ctx_len, sb.tiles,
                                    sb.ntiles, sb.nqt, sb.nsplit, self.scale, kv.k_scale[li], kv.v_scale[li])
         if self.w.fp8:

@@ -202,3 +202,26 @@ def test_engine_fused_decode_matches_unfused(monkeypatch):
     for a, b in zip(outs[0], outs[1]):
         for x, y in zip(a, b):
             assert x[:8] == y[:8]
+
+
+def test_rope_kv_write_kv_only_layout():
+    """Context-parallel gathered K/V rows ([T, 2*hkv*128], hq = 0, no q) are written like the K/V part of a full QKV
+    row (parallel/context_parallel.py)."""
+    from chronos import ops
+    from chronos.models.llama import get_config, rope_table
+
+    g = torch.Generator(device=DEV).manual_seed(11)
+    hq, hkv, T, nb, bs = 32, 8, 77, 16, 16
+    qkv = _rand(g, T, (hq + 2 * hkv) * 128)
+    cs = rope_table(get_config("llama3.1-8b"), 1024, DEV)
+    bt = torch.randperm(nb, device=DEV, generator=g).to(torch.int32).view(1, nb)
+    pos = torch.randperm(nb * bs, device=DEV, generator=g)[:T].to(torch.int32)
+    ts = torch.zeros(T, dtype=torch.int32, device=DEV)
+    k1, v1 = _rand(g, nb, hkv, bs, 128), _rand(g, nb, hkv, 128, bs)
+    k2, v2 = k1.clone(), v1.clone()
+    q = torch.empty(T, hq, 128, device=DEV, dtype=torch.bfloat16)
+    ops.rope_kv_write(qkv, pos, ts, bt, cs, q, k1, v1, hq, hkv, False)
+    kv_only = qkv[:, hq * 128:].contiguous()
+    ops.rope_kv_write(kv_only, pos, ts, bt, cs, q[:1], k2, v2, 0, hkv, False)
+    torch.cuda.synchronize()
+    assert torch.equal(k1, k2) and torch.equal(v1, v2)
