@@ -115,6 +115,27 @@ def build_constrain(force: bool = False) -> str:
     return _build("_constrain_native", srcs, ["g++"], flags, [], deps, force)
 
 
+def build_sanitize_harness(force: bool = False) -> str:
+    """The host C++ cores (sensor_core.h, token_dfa_core.h) linked into one test executable under AddressSanitizer +
+    UndefinedBehaviorSanitizer (GPU sanitizers are not available on the MI355X pool, so the
+    sanitizers cover the host code).  Returns the executable's path; run it to exercise both cores."""
+    src = os.path.join(CSRC, "tests", "host_sanitize.cpp")
+    deps = _deps([os.path.join(CSRC, "tests"), os.path.join(CSRC, "sensor_host"), os.path.join(CSRC, "constrain"),
+                  os.path.join(PKG_DIR, "sensor", "bpf")])
+    flags = ["-O1", "-g", "-std=c++17", "-Wall", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
+             "-fno-sanitize-recover=all"]
+    out = os.path.join(BUILD_DIR, "host_sanitize")
+    key = _hash([src] + deps, flags)
+    stamp = out + ".stamp"
+    if not force and os.path.exists(out) and os.path.exists(stamp) and open(stamp).read() == key:
+        return out
+    os.makedirs(BUILD_DIR, exist_ok=True)
+    _run(["g++"] + flags + [src, "-o", out])
+    with open(stamp, "w") as fh:
+        fh.write(key)
+    return out
+
+
 def hip_flags() -> tuple[list[str], list[str]]:
     import torch
 
