@@ -26,13 +26,47 @@ namespace chronos {
 constexpr int kD = 128;
 constexpr int kOStride = 132;  // LDS row stride (floats) of the merge buffer: breaks the 512-B row bank aliasing
 
+// One (tile, kv head)'s merge of the nsplit partial outputs (shared by the combine kernel and the in-launch combine).
+template <int NQT>
+__device__ __forceinline__ void combine_tile(const float* __restrict__ part_o, const float* __restrict__ part_lse,
+                                             uint16_t* __restrict__ out, int tile, int h, int rel0, int qbase,
+                                             int qlen, int hq, int hkv, int nsplit, int ntiles) {
+    constexpr int ROWS = NQT * 16;
+    const int G = hq / hkv;
+    for (int idx = threadIdx.x; idx < ROWS * 16; idx += 256) {
+        const int row = idx >> 4, c8 = idx & 15;
+        const int tr = rel0 + row / G, hd = h * G + row % G;
+        if (tr >= qlen) continue;
+        float M = -INFINITY;
+        for (int s = 0; s < nsplit; ++s)
+            M = fmaxf(M, part_lse[(((int64_t)s * ntiles + tile) * hkv + h) * ROWS + row]);
+        float L = 0.f, acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (M > -INFINITY) {
+            for (int s = 0; s < nsplit; ++s) {
+                const int64_t prow = (((int64_t)s * ntiles + tile) * hkv + h) * ROWS + row;
+                const float f = exp2f(part_lse[prow] - M);
+                if (f == 0.f) continue;
+                L += f;
+                const float* po = part_o + prow * kD + c8 * 8;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc[j] += po[j] * f;
+            }
+        }
+        const float inv = L > 0.f ? 1.f / L : 0.f;
+        u16x8 ov;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ov[j] = f2bf(acc[j] * inv);
+        *reinterpret_cast<u16x8*>(out + ((int64_t)(qbase + tr) * hq + hd) * kD + c8 * 8) = ov;
+    }
+}
+
 template <int NQT, bool FP8>
 __global__ void __launch_bounds__(256) paged_attn_kernel(
     const uint16_t* __restrict__ q, const void* __restrict__ kcv, const void* __restrict__ vcv,
     const int32_t* __restrict__ block_table, int bt_stride, const int32_t* __restrict__ q_start,
     const int32_t* __restrict__ ctx_len, const int32_t* __restrict__ tiles, uint16_t* __restrict__ out,
     float* __restrict__ part_o, float* __restrict__ part_lse, int hq, int hkv, int block_size, float scale_log2,
-    float k_scale, float v_scale, const int32_t* __restrict__ gst, int gn) {
+    float k_scale, float v_scale, const int32_t* __restrict__ gst, int gn, int* __restrict__ cnt) {
     constexpr int ROWS = NQT * 16;
     if (gate_closed(gst, gn)) return;
     const uint16_t* kc = reinterpret_cast<const uint16_t*>(kcv);
@@ -237,17 +271,38 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
             if (c8 == 0) part_lse[prow] = L > 0.f ? M + __log2f(L) : -INFINITY;
         }
     }
+    if (nsplit == 1 || cnt == nullptr) return;
+    // ---- in-launch flash-decoding combine: the last split of this (tile, head) to finish merges all of them ------
+    // cdna_hip_programming.md §5 "In-launch split-K reduction": every wave drains its partial stores, one agent-scope
+    // release, a relaxed agent-scope ticket; the last arriver resets the ticket, acquires, and reads every split's
+    // partials.  Correct for any placement of the splits over XCDs; saves the separate combine launch.
+    int* flag = reinterpret_cast<int*>(sm);  // the merge above is done with sm/sl/so after this barrier
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        int* c = cnt + (int64_t)tile * hkv + h;
+        const int old = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == nsplit - 1;
+        if (last) {
+            __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        flag[0] = last;
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+    combine_tile<NQT>(part_o, part_lse, out, tile, h, rel0, qbase, qlen, hq, hkv, nsplit, gridDim.x);
 }
-
-// Flash-decoding combine: out = sum_s 2^(lse_s - M) O_s / sum_s 2^(lse_s - M).
 template <int NQT>
 __global__ void __launch_bounds__(256) paged_attn_combine_kernel(
     const float* __restrict__ part_o, const float* __restrict__ part_lse, const int32_t* __restrict__ q_start,
     const int32_t* __restrict__ tiles, uint16_t* __restrict__ out, int hq, int hkv, int nsplit, int ntiles,
     const int32_t* __restrict__ gst, int gn) {
-    constexpr int ROWS = NQT * 16;
     if (gate_closed(gst, gn)) return;
-    const int tile = blockIdx.x, h = blockIdx.y, G = hq / hkv;
+    const int tile = blockIdx.x, h = blockIdx.y;
     int rel0, qbase, qlen;
     if (tiles) {
         const int seq = tiles[2 * tile];
@@ -259,31 +314,7 @@ __global__ void __launch_bounds__(256) paged_attn_combine_kernel(
         qbase = tile;
         qlen = 1;
     }
-    for (int idx = threadIdx.x; idx < ROWS * 16; idx += 256) {
-        const int row = idx >> 4, c8 = idx & 15;
-        const int tr = rel0 + row / G, hd = h * G + row % G;
-        if (tr >= qlen) continue;
-        float M = -INFINITY;
-        for (int s = 0; s < nsplit; ++s)
-            M = fmaxf(M, part_lse[(((int64_t)s * ntiles + tile) * hkv + h) * ROWS + row]);
-        float L = 0.f, acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (M > -INFINITY) {
-            for (int s = 0; s < nsplit; ++s) {
-                const int64_t prow = (((int64_t)s * ntiles + tile) * hkv + h) * ROWS + row;
-                const float f = exp2f(part_lse[prow] - M);
-                if (f == 0.f) continue;
-                L += f;
-                const float* po = part_o + prow * kD + c8 * 8;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) acc[j] += po[j] * f;
-            }
-        }
-        const float inv = L > 0.f ? 1.f / L : 0.f;
-        u16x8 ov;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) ov[j] = f2bf(acc[j] * inv);
-        *reinterpret_cast<u16x8*>(out + ((int64_t)(qbase + tr) * hq + hd) * kD + c8 * 8) = ov;
-    }
+    combine_tile<NQT>(part_o, part_lse, out, tile, h, rel0, qbase, qlen, hq, hkv, nsplit, ntiles);
 }
 
 // ------------------------------------------------------------------------------------------------------------------
@@ -463,6 +494,29 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
     }
 }
 
+// Split-completion tickets for the in-launch combine: one zeroed int per (tile, kv head), per device, allocated once by
+// attn_init() before any graph capture (hipMalloc is not capturable); every launch leaves them at zero again.
+constexpr int64_t kTicketCap = 1 << 20;
+static int* g_tickets[64] = {nullptr};
+
+void attn_init() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64 || g_tickets[dev]) return;
+    int* p = nullptr;
+    if (hipMalloc(&p, kTicketCap * sizeof(int)) != hipSuccess) return;
+    if (hipMemset(p, 0, kTicketCap * sizeof(int)) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        (void)hipFree(p);
+        return;
+    }
+    g_tickets[dev] = p;
+}
+
+static int* tickets_for(int64_t n) {
+    int dev = 0;
+    if (n > kTicketCap || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    return knob("attn_inkernel_combine", 1) ? g_tickets[dev] : nullptr;
+}
+
 size_t paged_attn_smem(int nqt) { return (size_t)(8 * nqt * 16 + 4 * nqt * 16 * kOStride) * sizeof(float); }
 
 void launch_paged_attn(const uint16_t* q, const void* kc, const void* vc, const int32_t* block_table, int bt_stride,
@@ -491,11 +545,12 @@ void launch_paged_attn(const uint16_t* q, const void* kc, const void* vc, const 
     }
 legacy:
     const dim3 grid(ntiles, hkv, nsplit), block(256);
+    int* cnt = nsplit > 1 ? tickets_for((int64_t)ntiles * hkv) : nullptr;
     const size_t sh = paged_attn_smem(nqt);
 #define PA_LAUNCH(N, F)                                                                                         \
     hipLaunchKernelGGL((paged_attn_kernel<N, F>), grid, block, sh, st, q, kc, vc, block_table, bt_stride, q_start, \
                        ctx_len, tiles, out, part_o, part_lse, hq, hkv, block_size, scale_log2, k_scale, v_scale, \
-                       CHRONOS_GATE)
+                       CHRONOS_GATE, cnt)
     if (nqt == 1) {
         if (fp8) PA_LAUNCH(1, true); else PA_LAUNCH(1, false);
     } else {
@@ -510,7 +565,7 @@ legacy:
         if (fp8) PA_LAUNCH(2, true); else PA_LAUNCH(2, false);
     }
 #undef PA_LAUNCH
-    if (nsplit > 1) {
+    if (nsplit > 1 && cnt == nullptr) {
         if (nqt == 1)
             hipLaunchKernelGGL(paged_attn_combine_kernel<1>, dim3(ntiles, hkv), block, 0, st, part_o, part_lse,
                                q_start, tiles, out, hq, hkv, nsplit, ntiles, CHRONOS_GATE);

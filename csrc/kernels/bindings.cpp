@@ -35,6 +35,7 @@ void launch_constrained_sample(const void*, bool, int64_t, const int32_t*, int, 
                                int, int32_t*, int32_t*, const float*, const int32_t*, const int32_t*, const float*,
                                int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, int, hipStream_t);
 void launch_gemv(const uint16_t*, int, int, const uint16_t*, int, uint16_t*, bool, hipStream_t);
+void attn_init();
 void launch_gemm(const uint16_t*, const uint16_t*, uint16_t*, int, int, int, bool, int, hipStream_t);
 void* ar_create(int, int, int64_t);
 std::vector<uint8_t> ar_handles(void*);
@@ -520,6 +521,7 @@ TORCH_LIBRARY(chronos, m) {
           "Tensor block_table, Tensor cos_sin, Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, int hq, "
           "int hkv, float k_scale=1.0, float v_scale=1.0) -> ()");
     m.def("set_decode_gate(Tensor? state, int n) -> ()", &set_decode_gate);
+    m.def("attn_init() -> ()", [] { chronos::attn_init(); });
     m.def("quant_rows(Tensor x, Tensor(a!)? resid, Tensor? w, float eps, int mode) -> (Tensor, Tensor)");
     m.def("qlinear(Tensor xq, Tensor xs, Tensor wq, Tensor ws, bool swiglu) -> Tensor");
     m.def("set_knob(str name, int value) -> ()", &set_knob);

@@ -151,6 +151,7 @@ class Engine:
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
             ops.load()  # the HIP library must load on a GPU engine — never a silent eager fallback
+            ops.device_init()
         self.tok = tokenizer or load_tokenizer(cfg.tokenizer)
         t0 = time.perf_counter()
         self.model = model or build_model(cfg.model, self.device, self.tp, cfg.seed, cfg.checkpoint,

@@ -27,11 +27,19 @@ def load() -> None:
 
         kernels_lib()
         _loaded = True
+        if torch.cuda.is_available():
+            torch.ops.chronos.attn_init()  # current device; Engine repeats it after selecting its own
 
 
 def _k():
     load()
     return torch.ops.chronos
+
+
+def device_init() -> None:
+    """Per-device kernel state for the current HIP device (the attention kernel's split-completion tickets); call
+    after set_device and before any graph capture.  Idempotent."""
+    _k().attn_init()
 
 
 def embedding(ids: torch.Tensor, table: torch.Tensor, vstart: int = 0) -> torch.Tensor:

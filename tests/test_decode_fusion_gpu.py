@@ -225,3 +225,46 @@ def test_rope_kv_write_kv_only_layout():
     ops.rope_kv_write(kv_only, pos, ts, bt, cs, q[:1], k2, v2, 0, hkv, False)
     torch.cuda.synchronize()
     assert torch.equal(k1, k2) and torch.equal(v1, v2)
+
+
+@pytest.mark.parametrize("nsplit", [2, 5])
+def test_inlaunch_combine_matches_combine_kernel_and_replays(nsplit):
+    """Split-K decode attention with the last-arriver combine inside the launch == the separate combine kernel (same
+    merge code, so bit-exact), and the split tickets return to zero: a captured graph replays correctly."""
+    from chronos import ops
+
+    g = torch.Generator(device=DEV).manual_seed(nsplit)
+    hq, hkv, bs, B = 32, 8, 16, 6
+    ctx = [700, 33, 1, 480, 1024, 260]
+    nb = sum((c + bs - 1) // bs for c in ctx) + 2
+    k, v = _rand(g, nb, hkv, bs, 128), _rand(g, nb, hkv, 128, bs)
+    perm = torch.randperm(nb, generator=torch.Generator().manual_seed(1)).tolist()
+    bt = torch.zeros(B, 64, dtype=torch.int32)
+    o = 0
+    for b, c in enumerate(ctx):
+        n = (c + bs - 1) // bs
+        bt[b, :n] = torch.tensor(perm[o:o + n])
+        o += n
+    bt = bt.to(DEV)
+    q = _rand(g, B, hq, 128, scale=2.0)
+    qs = torch.arange(B + 1, dtype=torch.int32, device=DEV)
+    cl = torch.tensor(ctx, dtype=torch.int32, device=DEV)
+    run = lambda: ops.paged_attention(q, k, v, bt, qs, cl, None, B, 1, nsplit)  # noqa: E731
+    torch.ops.chronos.set_knob("attn_inkernel_combine", 0)
+    try:
+        ref = run()
+    finally:
+        torch.ops.chronos.set_knob("attn_inkernel_combine", 1)
+    out = run()
+    assert torch.equal(out, ref)
+    static = torch.empty_like(ref)
+    graph = torch.cuda.CUDAGraph()
+    run()
+    torch.cuda.synchronize()
+    with torch.cuda.graph(graph):
+        static.copy_(run())
+    for _ in range(3):
+        static.zero_()
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(static, ref)
