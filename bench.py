@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--model", default="llama3-8b")
     ap.add_argument("--streams", type=int, default=1024, help="concurrent sensor streams (chains per step) per GPU")
     ap.add_argument("--num-predict", type=int, default=64)
-    ap.add_argument("--single-stream", type=int, default=8, help="chains for the single-stream p50 latency")
+    ap.add_argument("--single-stream", type=int, default=16, help="chains for the single-stream p50 latency")
     ap.add_argument("--burst", type=int, default=8)
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-prefix-cache", action="store_true")
@@ -195,9 +195,12 @@ def main():
     for p in prompts[a.streams * per_stream:]:
         single += run_step([p])
     single_lat = [r.latency for r in single[1:]] or [r.latency for r in single]
+    # per-token decode time of the single stream: independent of how long the random-weight verdicts happen to be
+    ss = single[1:] or single
+    single_tok = [((r.t_done - r.t_first), len(r.out_ids)) for r in ss if r.t_first]
 
     stats = dict(elapsed=elapsed, ok=ok, n=len(timed), lat=lat, gen=gen_tok, ptok=prompt_tok, single=single_lat,
-                 hits=hits, tp_rank=tp_rank)
+                 single_tok=single_tok, hits=hits, tp_rank=tp_rank)
     if world > 1:
         allst = [None] * world
         dist.all_gather_object(allst, stats)
@@ -240,6 +243,11 @@ def main():
             "p50_verdict_latency_ms": round(1000 * statistics.median(lats), 2),
             "p99_verdict_latency_ms": round(1000 * sorted(lats)[max(0, math.ceil(0.99 * len(lats)) - 1)], 2),
             "single_stream_p50_latency_ms": round(1000 * statistics.median(singles), 2) if singles else None,
+            "single_stream_decode_ms_per_token": round(
+                1000 * sum(t for s in allst for t, _ in s["single_tok"])
+                / max(1, sum(n for s in allst for _, n in s["single_tok"])), 3),
+            "single_stream_verdict_tokens": round(
+                sum(n for s in allst for _, n in s["single_tok"]) / max(1, sum(len(s["single_tok"]) for s in allst)), 1),
             "verdicts_valid": f"{oks}/{n}",
             "prompt_tokens_per_chain": round(sum(s["ptok"] for s in allst) / n, 1),
             "verdict_tokens_per_chain": round(sum(s["gen"] for s in allst) / n, 1),

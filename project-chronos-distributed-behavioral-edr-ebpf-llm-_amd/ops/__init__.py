@@ -18,6 +18,40 @@ from .gemm import LazyNorm, ResidOut, gate_up_silu, gemv_ok, gemv_resid, linear,
 
 _loaded = False
 
+# Debug-mode device-index validation: GPU AddressSanitizer is not available on the MI355X pool, and an
+# out-of-bounds paged-KV access can fault the whole GPU, so with CHRONOS_CHECK_INPUTS=1 every index a hand-written
+# kernel will dereference (block-table entries, positions, slots, grammar states, tiles) is range-checked on the host
+# BEFORE the launch and a bad one raises IndexError instead.  Costs a device->host copy per op: a debug mode (skipped
+# inside graph capture, where a copy would break the capture; the eager steps exercise the same indices).
+_CHECK = os.environ.get("CHRONOS_CHECK_INPUTS", "0") not in ("", "0")
+
+
+def set_input_checks(on: bool) -> None:
+    global _CHECK
+    _CHECK = bool(on)
+
+
+def _checking(t: torch.Tensor) -> bool:
+    return _CHECK and t.is_cuda and not torch.cuda.is_current_stream_capturing()
+
+
+def _need(cond: bool, what: str) -> None:
+    if not cond:
+        raise IndexError(f"chronos input check: {what}")
+
+
+def _check_paged(block_table, k_cache, tok_rows, kv_len, what: str) -> None:
+    """Every cache block a kernel can touch exists: rows tok_rows of block_table over the first kv_len tokens."""
+    bt = block_table.cpu()
+    nb, bs = k_cache.shape[0], k_cache.shape[2]
+    rows = tok_rows.cpu().long()
+    lens = kv_len.cpu().long()
+    _need(bool(((rows >= 0) & (rows < bt.shape[0])).all()), f"{what}: block-table row out of range")
+    _need(bool(((lens >= 0) & ((lens + bs - 1) // bs <= bt.shape[1])).all()), f"{what}: length exceeds block table")
+    for r, n in zip(rows.tolist(), lens.tolist()):
+        used = bt[r, :(n + bs - 1) // bs]
+        _need(bool(((used >= 0) & (used < nb)).all()), f"{what}: block id out of range in row {r}")
+
 
 def load() -> None:
     """Load (building in-tree if stale) the HIP kernel library; raises on failure."""
@@ -119,6 +153,10 @@ def qgate_up_quant(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: tor
 def rope_kv_write(qkv, pos, tok_seq, block_table, cos_sin, q_out, k_cache, v_cache, hq: int, hkv: int,
                   write_q: bool = True, k_scale: float = 1.0, v_scale: float = 1.0) -> None:
     """RoPE q/k + write k/v into the paged cache (bf16, or fp8-e4m3 bytes when the cache is uint8)."""
+    if _checking(qkv):
+        p = pos.cpu().long()
+        _need(bool(((p >= 0) & (p < cos_sin.shape[0])).all()), "rope_kv_write: position outside the rope table")
+        _check_paged(block_table, k_cache, tok_seq, p + 1, "rope_kv_write")
     if qkv.is_cuda:
         _k().rope_kv_write(qkv, pos, tok_seq, block_table, cos_sin, q_out, k_cache, v_cache, hq, hkv, write_q,
                            k_scale, v_scale)
@@ -157,6 +195,16 @@ def paged_attention(q, k_cache, v_cache, block_table, q_start, ctx_len, tiles=No
                     nsplit: int = 1, scale: float | None = None, k_scale: float = 1.0,
                     v_scale: float = 1.0) -> torch.Tensor:
     scale = scale if scale is not None else 1.0 / math.sqrt(q.shape[-1])
+    if _checking(q):
+        nseq = ctx_len.shape[0] if tiles is None else q_start.shape[0] - 1
+        if tiles is None:
+            _need(ntiles <= ctx_len.shape[0] and ntiles <= q.shape[0], "paged_attention: decode rows")
+        else:
+            tl = tiles.cpu().long()
+            _need(bool(((tl[:, 0] >= 0) & (tl[:, 0] < nseq)).all()), "paged_attention: tile sequence out of range")
+            qs = q_start.cpu().long()
+            _need(bool((qs[1:] >= qs[:-1]).all()) and int(qs[-1]) <= q.shape[0], "paged_attention: q_start")
+        _check_paged(block_table, k_cache, torch.arange(nseq), ctx_len[:nseq], "paged_attention")
     if q.is_cuda:
         return _k().paged_attention(q, k_cache, v_cache, block_table, q_start, ctx_len, tiles, ntiles, nqt, nsplit,
                                     scale, k_scale, v_scale)
@@ -166,6 +214,15 @@ def paged_attention(q, k_cache, v_cache, block_table, q_start, ctx_len, tiles=No
 
 def constrained_sample(logits, row_of_slot, next_tab, dist, done_state: int, state, remaining, temperature, seed,
                        ids, pos, ctx, nout, out_tokens, topk=None, topp=None) -> None:
+    if _checking(logits):
+        st = state.cpu().long()
+        _need(bool(((st >= -1) & (st < next_tab.shape[0])).all()), "constrained_sample: grammar state out of range")
+        _need(next_tab.shape[1] <= logits.shape[-1], "constrained_sample: grammar table wider than the logits")
+        if row_of_slot is not None:
+            rs = row_of_slot.cpu().long()
+            _need(bool(((rs >= -1) & (rs < logits.shape[0])).all()), "constrained_sample: logits row out of range")
+        else:
+            _need(state.shape[0] <= logits.shape[0], "constrained_sample: more slots than logits rows")
     if logits.is_cuda:
         _k().constrained_sample(logits, row_of_slot, next_tab, dist, done_state, state, remaining, temperature, seed,
                                 ids, pos, ctx, nout, out_tokens, topk, topp)

@@ -268,3 +268,42 @@ def test_inlaunch_combine_matches_combine_kernel_and_replays(nsplit):
         graph.replay()
         torch.cuda.synchronize()
         assert torch.equal(static, ref)
+
+
+def test_input_checks_catch_bad_indices_before_launch():
+    """CHRONOS_CHECK_INPUTS debug mode: a block id past the cache, a position past the rope table or a stray grammar
+    state raise IndexError on the host instead of reaching a kernel; good inputs pass; an engine runs with it on."""
+    from chronos import ops
+    from chronos.models.llama import get_config, rope_table
+
+    g = torch.Generator(device=DEV).manual_seed(5)
+    hq, hkv, nb, bs, T = 8, 2, 6, 16, 3
+    cs = rope_table(get_config("llama3-8b"), 64, DEV)
+    qkv = _rand(g, T, (hq + 2 * hkv) * 128)
+    k, v = _rand(g, nb, hkv, bs, 128), _rand(g, nb, hkv, 128, bs)
+    q = torch.empty(T, hq, 128, device=DEV, dtype=torch.bfloat16)
+    ts = torch.zeros(T, dtype=torch.int32, device=DEV)
+    pos = torch.tensor([0, 17, 40], dtype=torch.int32, device=DEV)
+    ops.set_input_checks(True)
+    try:
+        good = torch.tensor([[1, 2, 3, 0]], dtype=torch.int32, device=DEV)
+        ops.rope_kv_write(qkv, pos, ts, good, cs, q, k, v, hq, hkv)
+        bad = torch.tensor([[1, 2, 99, 0]], dtype=torch.int32, device=DEV)  # block 99 of a 6-block cache
+        with pytest.raises(IndexError):
+            ops.rope_kv_write(qkv, pos, ts, bad, cs, q, k, v, hq, hkv)
+        with pytest.raises(IndexError):  # position 500 is past the 64-row rope table
+            ops.rope_kv_write(qkv, torch.tensor([0, 1, 500], dtype=torch.int32, device=DEV), ts, good, cs, q, k, v,
+                              hq, hkv)
+        qs = torch.arange(2, dtype=torch.int32, device=DEV)
+        with pytest.raises(IndexError):
+            ops.paged_attention(q[:1], k, v, bad, qs, torch.tensor([41], dtype=torch.int32, device=DEV), None, 1)
+        from chronos.brain.engine.engine import Engine, EngineConfig
+        from chronos.sensor.prompt import VERDICT_SCHEMA, build_prompt
+
+        eng = Engine(EngineConfig(model="small", device=DEV, max_slots=2, max_model_len=256, use_graphs=False))
+        r = eng.submit(build_prompt(["[EXEC] bash -> curl", "[OPEN] curl -> /tmp/x"]), fmt=VERDICT_SCHEMA,
+                       num_predict=16)
+        eng.run_until_idle()
+        assert r.done_reason in ("stop", "length") and r.out_ids
+    finally:
+        ops.set_input_checks(False)
