@@ -7,7 +7,10 @@ Routing is by measured shape (profiles/r1_gemm_vs_hipblaslt.json, cold weights, 
   streaming — beats hipBLASLt on every decode shape;
 * gate_up at 3 <= M <= 128: the MFMA GEMM with the fused SwiGLU epilogue (csrc/kernels/gemm.hip) — 1.05-1.24x over
   hipBLASLt + the separate silu_mul pass, which it removes;
-* everything else: hipBLASLt via torch.matmul (the "plain library GEMM" rule).  The hand-written 128x128-tile MFMA
+* everything else: hipBLASLt via torch.matmul (the "plain library GEMM" rule).  Measured alternatives that did not
+  pay at the wave's M = 1024 decode bucket: a TunableOp sweep over every library solution (~1 % of the wave,
+  profiles/r1s4_tunableop_gemm_study.jsonl) and two half-batches on two HIP streams so the under-filled N = 4096 /
+  6144 projections run side by side (-2 % decode GPU time, but a slower wave: 580 vs 608 chains/s).  The hand-written 128x128-tile MFMA
   GEMM loses there: one tile per CU is bound by the per-CU load path (~0.7 us per 64-deep K-step), the same wall
   hipBLASLt's 128x128 tiles hit, and it has no answer to the small-grid shapes (N = 4096 at M <= 128).
 """
