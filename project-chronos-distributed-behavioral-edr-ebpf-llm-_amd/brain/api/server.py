@@ -180,7 +180,11 @@ def main(argv=None) -> int:
     ap.add_argument("--tokenizer", default=None)
     ap.add_argument("--served-name", default="llama3")
     ap.add_argument("--dp", type=int, default=1, help="engine replicas, one process per GPU")
-    ap.add_argument("--tp", type=int, default=1, help="tensor-parallel degree per replica (torchrun launch)")
+    ap.add_argument("--tp", type=int, default=1,
+                    help="tensor-parallel degree (launch with torchrun --nproc-per-node TP: rank 0 serves HTTP, the "
+                         "other ranks follow the lockstep scheduler)")
+    ap.add_argument("--cp", type=int, default=1,
+                    help="context-parallel degree for long kill-chain prefill (torchrun launch, full weights per rank)")
     ap.add_argument("--max-slots", type=int, default=512)
     ap.add_argument("--max-model-len", type=int, default=4096)
     ap.add_argument("--device", default="cuda")
@@ -205,7 +209,29 @@ def main(argv=None) -> int:
         cfg = EngineConfig(model=a.model, checkpoint=a.checkpoint, tokenizer=a.tokenizer, device=a.device,
                            max_slots=a.max_slots, max_model_len=a.max_model_len, kv_dtype=a.kv_dtype,
                            request_timeout_s=a.request_timeout)
-        if a.dp > 1:
+        if a.tp > 1 or a.cp > 1:
+            if a.tp > 1 and a.cp > 1:
+                raise SystemExit("--tp and --cp are exclusive (CP ranks hold full weights)")
+            import os
+
+            from ...parallel.tp import TPContext
+            from ...parallel.tp_engine import TPEngine, init_tp
+            from .service import LockstepService
+
+            if a.device == "cuda":  # before the process group: RCCL and the IPC all-reduce bind the current device
+                import torch
+
+                torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+            grp, ctrl = init_tp("nccl" if a.device == "cuda" else "gloo", ipc_allreduce=None if a.tp > 1 else False)
+            want = a.tp if a.tp > 1 else a.cp
+            if grp.world != want:
+                raise SystemExit(f"world size {grp.world} != {'--tp' if a.tp > 1 else '--cp'} {want}")
+            tpe = TPEngine(cfg, grp, ctrl) if a.tp > 1 else TPEngine(cfg, TPContext.single(), ctrl, cp=grp)
+            if grp.rank != 0:
+                tpe.follower_loop()  # until the leader shuts down
+                return 0
+            backend = LockstepService(tpe, a.served_name)
+        elif a.dp > 1:
             from ...parallel.router import DPRouter
 
             backend = DPRouter(cfg, a.dp)

@@ -189,3 +189,65 @@ class EngineService:
             "waiting": len(eng.waiting),
             "stats": dict(eng.stats),
         }
+
+
+class LockstepService(EngineService):
+    """The HTTP-facing service of a TP (or CP) group's leader rank: the same asyncio API and watchdog as
+    EngineService, but requests enter the lockstep scheduler (parallel/tp_engine.py TPEngine) and the scheduler
+    thread steps it continuously — an idle step is the followers' heartbeat (they block in the step's broadcast).
+    Incremental token streaming is not offered here: a stream=true request gets its text in one piece at the end."""
+
+    def __init__(self, tpe, model_name: str = "llama3", step_deadline_s: float = 120.0, idle_s: float = 0.02):
+        self.tpe = tpe
+        self.idle_s = idle_s
+        super().__init__(tpe.engine, model_name, step_deadline_s)
+
+    def _loop(self) -> None:
+        while not self._stop.is_set():
+            while True:
+                try:
+                    self._handle(self._q.get_nowait())
+                except queue.Empty:
+                    break
+            busy = self.engine.has_work()
+            t = self._step_t0 = time.perf_counter()
+            try:
+                done, _ = self.tpe.step()
+            except Exception as e:
+                log.exception("lockstep step failed")
+                self.last_error = f"{type(e).__name__}: {e}"
+                self.stalled = True
+                self._step_t0 = None
+                time.sleep(self.idle_s)
+                continue
+            self._step_t0 = None
+            if busy:
+                METRICS.observe_step(time.perf_counter() - t, self.engine)
+            for r in done:
+                METRICS.observe_request(r)
+            if not busy:
+                time.sleep(self.idle_s)
+        try:  # release the followers
+            self.tpe.step(stop=True)
+        except Exception:  # noqa: BLE001 — shutting down
+            pass
+
+    def _handle(self, item) -> None:
+        kind = item[0]
+        if kind == "submit":
+            _, params, ids, on_done, _on_tokens, handle = item
+            if handle.get("cancelled"):
+                return
+            handle["tag"] = self.tpe.submit(ids, fmt=params.format, num_predict=params.num_predict,
+                                            temperature=params.temperature, seed=params.seed, callback=on_done,
+                                            top_k=params.top_k, top_p=params.top_p)
+        elif kind == "cancel":
+            tag = item[1].get("tag")
+            if tag is not None:
+                self.tpe.cancel(tag)
+
+    async def generate_stream(self, params: GenerateParams) -> AsyncIterator[tuple[str, Optional[Request]]]:
+        req = await self.generate(params)
+        if req.text:
+            yield req.text, None
+        yield "", req

@@ -36,6 +36,8 @@ class _Sub:
     temperature: float = 0.0
     seed: int = 0
     tag: int = 0
+    top_k: int = 0
+    top_p: float = 1.0
 
 
 @dataclass
@@ -46,14 +48,20 @@ class _Msg:
 
 
 class TPEngine:
-    def __init__(self, cfg: EngineConfig, tp: TPContext, ctrl_group=None):
+    """Lockstep replicated scheduler over a TP group — or, with ``cp``, over a context-parallel group of full-weight
+    ranks (parallel/context_parallel.py); the control plane is the same."""
+
+    def __init__(self, cfg: EngineConfig, tp: TPContext, ctrl_group=None, cp: TPContext | None = None):
         from dataclasses import replace
 
-        self.tp = tp
-        self.ctrl = ctrl_group  # gloo group spanning the TP ranks (host-side control plane)
+        self.tp = tp if cp is None else cp  # the lockstep group
+        self.ctrl = ctrl_group  # gloo group spanning the lockstep ranks (host-side control plane)
         self.timeout_s = cfg.request_timeout_s  # enforced by the leader only (module docstring)
-        self.engine = Engine(replace(cfg, request_timeout_s=0.0), tp=tp)
-        self.leader = tp.rank == 0
+        if cp is None:
+            self.engine = Engine(replace(cfg, request_timeout_s=0.0), tp=tp)
+        else:
+            self.engine = Engine(replace(cfg, request_timeout_s=0.0), cp=cp)
+        self.leader = self.tp.rank == 0
         self._inbox: "queue.Queue[_Sub]" = queue.Queue()
         self._cancel_inbox: "queue.Queue[tuple[int, str]]" = queue.Queue()
         self._callbacks: dict[int, Callable[[Request], None]] = {}
@@ -63,7 +71,7 @@ class TPEngine:
 
     # ---- leader API ----------------------------------------------------------------------------------------------
     def submit(self, prompt, fmt=None, num_predict: int | None = None, temperature: float = 0.0, seed: int = 0,
-               callback: Callable[[Request], None] | None = None) -> int:
+               callback: Callable[[Request], None] | None = None, top_k: int = 0, top_p: float = 1.0) -> int:
         assert self.leader, "requests enter through TP rank 0"
         ids = prompt if isinstance(prompt, list) else self.engine.tok.chat_ids(prompt)
         with self._lock:
@@ -71,7 +79,7 @@ class TPEngine:
             tag = self._tag
             if callback is not None:
                 self._callbacks[tag] = callback
-        self._inbox.put(_Sub(ids, fmt, num_predict, temperature, seed, tag))
+        self._inbox.put(_Sub(ids, fmt, num_predict, temperature, seed, tag, top_k, top_p))
         return tag
 
     def cancel(self, tag: int, reason: str = "cancelled") -> None:
@@ -108,7 +116,7 @@ class TPEngine:
         for s in msg.subs:
             cb = self._callbacks.pop(s.tag, None) if self.leader else None
             r = self.engine.submit(s.ids, fmt=s.fmt, num_predict=s.num_predict, temperature=s.temperature,
-                                   seed=s.seed, callback=cb, meta={"tag": s.tag})
+                                   seed=s.seed, callback=cb, meta={"tag": s.tag}, top_k=s.top_k, top_p=s.top_p)
             if not r.done_reason:
                 self._reqs[s.tag] = r
         for tag, reason in msg.cancels:

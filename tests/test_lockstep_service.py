@@ -1,0 +1,83 @@
+"""The HTTP-facing lockstep service of a TP / CP group (brain/api/service.py LockstepService) over gloo, world 2:
+requests submitted through the leader's asyncio API come back as valid verdicts (incl. a long prompt that takes the
+context-parallel path), the follower stays in lockstep and is released when the leader's service closes."""
+import json
+import os
+import socket
+
+import pytest
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, mode, q):
+    import asyncio
+
+    import torch.distributed as dist
+
+    from chronos.brain.api.protocol import GenerateParams
+    from chronos.brain.api.service import LockstepService
+    from chronos.brain.engine.engine import EngineConfig
+    from chronos.parallel.tp import TPContext
+    from chronos.parallel.tp_engine import TPEngine
+    from chronos.sensor.prompt import VERDICT_SCHEMA, build_prompt
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    grp = TPContext.from_group()
+    cfg = EngineConfig(model="tiny", device="cpu", max_slots=4, max_model_len=1024, use_graphs=False,
+                       decode_burst=4, max_prefill_tokens=128, cp_min_tokens=64)
+    tpe = TPEngine(cfg, grp, None) if mode == "tp" else TPEngine(cfg, TPContext.single(), None, cp=grp)
+    if rank != 0:
+        tpe.follower_loop()
+        q.put((rank, dict(tpe.engine.stats)))
+    else:
+        svc = LockstepService(tpe, "llama3", idle_s=0.005)
+        long_hist = [f"[OPEN] bash -> /var/lib/app/f{i}.dat" for i in range(30)] + ["[EXEC] bash -> curl"]
+        prompts = [build_prompt(["[OPEN] attack_chain.sh -> /tmp/malware.bin", "[EXEC] attack_chain.sh -> curl"]),
+                   build_prompt(long_hist)]
+
+        async def go():
+            ps = [GenerateParams(model="llama3", prompt=p, format=VERDICT_SCHEMA, num_predict=24) for p in prompts]
+            reqs = await asyncio.gather(*[svc.generate(p) for p in ps])
+            chunks = [c async for c in svc.generate_stream(ps[0])]
+            return reqs, chunks
+
+        reqs, chunks = asyncio.run(go())
+        svc.close()
+        q.put((0, [r.text for r in reqs], chunks[-1][1].text, dict(tpe.engine.stats)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("mode", ["tp", "cp"])
+def test_lockstep_service_world2(mode):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, mode, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(2):
+        item = q.get(timeout=600)
+        res[item[0]] = item
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    _, texts, streamed, stats = res[0]
+    for t in texts + [streamed]:
+        v = json.loads(t)
+        assert {"risk_score", "verdict", "reason"} <= set(v)
+    assert res[1][1]["completed"] == stats["completed"] == 3  # the follower ran the same requests in lockstep
+    if mode == "cp":
+        assert stats["cp_prefill_steps"] >= 1
