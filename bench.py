@@ -55,6 +55,8 @@ def parse():
                     help="tensor-parallel degree per replica (e.g. --model llama3-70b --tp 8): the world is split into "
                          "world/tp replicas, each a lockstep TP engine over RCCL (+ the IPC one-shot all-reduce)")
     ap.add_argument("--max-model-len", type=int, default=512)
+    ap.add_argument("--sequence-parallel", action="store_true",
+                    help="with --tp: Megatron sequence parallelism in prefill (reduce-scatter / all-gather)")
     return ap.parse_args()
 
 
@@ -129,7 +131,7 @@ def main():
     cfg = EngineConfig(model=a.model, device=str(device), max_slots=a.streams, max_model_len=a.max_model_len,
                        default_num_predict=a.num_predict, decode_burst=a.burst, use_graphs=not a.no_graphs,
                        prefix_cache=not a.no_prefix_cache, async_harvest=a.async_harvest, seed=0,
-                       weight_dtype=a.weights)
+                       weight_dtype=a.weights, tp_sequence_parallel=a.sequence_parallel)
     # TP: the ranks of a replica submit the same chains in the same order and step the same deterministic scheduler,
     # so they stay in lockstep by construction (the serving path adds the leader broadcast of parallel/tp_engine.py)
     eng = Engine(cfg, tp=tp)

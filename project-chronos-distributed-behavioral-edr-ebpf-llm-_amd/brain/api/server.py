@@ -183,6 +183,7 @@ def main(argv=None) -> int:
     ap.add_argument("--tp", type=int, default=1,
                     help="tensor-parallel degree (launch with torchrun --nproc-per-node TP: rank 0 serves HTTP, the "
                          "other ranks follow the lockstep scheduler)")
+    ap.add_argument("--sequence-parallel", action="store_true", help="with --tp: sequence-parallel prefill")
     ap.add_argument("--cp", type=int, default=1,
                     help="context-parallel degree for long kill-chain prefill (torchrun launch, full weights per rank)")
     ap.add_argument("--max-slots", type=int, default=512)
@@ -208,7 +209,7 @@ def main(argv=None) -> int:
 
         cfg = EngineConfig(model=a.model, checkpoint=a.checkpoint, tokenizer=a.tokenizer, device=a.device,
                            max_slots=a.max_slots, max_model_len=a.max_model_len, kv_dtype=a.kv_dtype,
-                           request_timeout_s=a.request_timeout)
+                           request_timeout_s=a.request_timeout, tp_sequence_parallel=a.sequence_parallel)
         if a.tp > 1 or a.cp > 1:
             if a.tp > 1 and a.cp > 1:
                 raise SystemExit("--tp and --cp are exclusive (CP ranks hold full weights)")

@@ -74,6 +74,7 @@ class EngineConfig:
     request_timeout_s: float = 0.0  # >0: a request not finished this long after submit is cancelled (reason "timeout")
     tp_overlap: bool = True        # TP prefill: two micro-batches, each one's RCCL all-reduces overlap the other's compute
     tp_overlap_min_tokens: int = 1024
+    tp_sequence_parallel: bool = False  # TP prefill: reduce-scatter / all-gather around the norms instead of all-reduce
     decode_gate: bool = True       # small buckets: kernels of steps after the last live row finished return at once
     cp_min_tokens: int = 4096      # context parallel (Engine(cp=...)): prefill chunks at least this long are split
 
@@ -157,6 +158,7 @@ class Engine:
         self.model = model or build_model(cfg.model, self.device, self.tp, cfg.seed, cfg.checkpoint,
                                           max_position=cfg.max_model_len + 16, weight_dtype=cfg.weight_dtype)
         self.load_seconds = time.perf_counter() - t0
+        self.model.sequence_parallel = cfg.tp_sequence_parallel and self.tp.world > 1
         mc = self.model.cfg
         self.bank = GrammarBank(self.tok.token_bytes_list(), self.tok.stop_ids, mc.vocab_size, cfg.grammar_capacity,
                                 self.device, max_string=cfg.max_string)

@@ -547,6 +547,8 @@ class LlamaModel:
         self.hq, self.hkv = _local_heads(cfg, self.tp)
         self.cos_sin = rope_table(cfg, max_position or cfg.max_position, self.device)
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
+        # Megatron-style sequence parallelism for TP prefill (set by the engine, EngineConfig.tp_sequence_parallel)
+        self.sequence_parallel = False
 
     # ---- one micro-batch's pieces of a layer (bf16: x is a tensor; W8A8: x is (e4m3 bytes, row scales)) ----------
     def _norm(self, h, st: dict, w: torch.Tensor, first: bool = False):
@@ -602,6 +604,32 @@ class LlamaModel:
             return ops.qlinear(*ops.qgate_up_quant(*x, lw.w_gu.q, lw.w_gu.s), lw.w_down.q, lw.w_down.s)
         return self._out_proj(ops.gate_up_silu(x, lw.w_gu), lw.w_down, st)
 
+    def _forward_sp(self, sb: StepBatch, kv: KVCache, logits_dtype) -> torch.Tensor:
+        """TP prefill with sequence parallelism (SURVEY.md §2.5 "Sequence parallel"): every row-parallel output is
+        reduce-SCATTERED over the token rows instead of all-reduced, so the residual stream lives sharded ([T/W, d]
+        per rank) and each rank adds + normalises only its own rows; the normalised rows are all-gathered in front
+        of the next column-parallel GEMM.  Same bytes on the wire as the all-reduce form, 1/W of the norm/residual
+        work and memory.  T is padded to a multiple of W with zero rows (dropped before the projections)."""
+        cfg, w, tp = self.cfg, self.w, self.tp
+        T = sb.ids.numel()
+        Tp = -(-T // tp.world) * tp.world
+        eps = cfg.rms_eps
+        emb = ops.embedding(sb.ids, w.embed, w.vocab_start)
+        resid = tp.reduce_scatter_rows(_pad_rows(emb, Tp))  # vocab-parallel embedding: partial rows -> shard
+        st = dict(sb=sb, T=T, resid=resid, q_buf=torch.empty(T, self.hq, cfg.head_dim, device=emb.device,
+                                                             dtype=emb.dtype))
+        xs = ops.rmsnorm(resid, w.layers[0].attn_norm, eps)
+        L = len(w.layers)
+        for li, lw in enumerate(w.layers):
+            st["x"] = tp.all_gather_rows(xs)[:T]
+            o = tp.reduce_scatter_rows(_pad_rows(self._attn(li, lw, st, kv), Tp))
+            st["x"] = tp.all_gather_rows(ops.add_rmsnorm(o, st["resid"], lw.mlp_norm, eps))[:T]
+            dn = tp.reduce_scatter_rows(_pad_rows(self._mlp(lw, st), Tp))
+            xs = ops.add_rmsnorm(dn, st["resid"], w.layers[li + 1].attn_norm if li + 1 < L else w.norm, eps)
+        x = tp.all_gather_rows(xs)[:T].index_select(0, sb.last_idx)
+        logits = tp.all_gather_last(ops.linear(x, w.lm_head))
+        return logits if logits.dtype == logits_dtype else logits.to(logits_dtype)
+
     def forward(self, sb: StepBatch, kv: KVCache, logits_dtype=torch.bfloat16) -> torch.Tensor:
         """Returns logits [B, V] for the token at sb.last_idx of every sequence (full vocab on every TP rank).
 
@@ -612,6 +640,8 @@ class LlamaModel:
         Single part (decode, TP=1): the same ops in the same order with synchronous all-reduces (graph-capturable, the
         IPC one-shot kernel for decode-sized messages)."""
         cfg, w, tp = self.cfg, self.w, self.tp
+        if tp.world > 1 and sb.tiles is not None and self.sequence_parallel and not w.fp8 and sb.cp is None:
+            return self._forward_sp(sb, kv, logits_dtype)
         parts = sb.parts if (sb.parts and tp.world > 1) else [sb]
         overlap = len(parts) > 1
         ar = (lambda t: tp.all_reduce_async(t)) if overlap else (lambda t: (tp.all_reduce(t), None))  # noqa: E731
@@ -646,6 +676,14 @@ class LlamaModel:
         logits = ops.linear(x, w.lm_head)
         logits = tp.all_gather_last(logits)
         return logits if logits.dtype == logits_dtype else logits.to(logits_dtype)
+
+
+def _pad_rows(x: torch.Tensor, rows: int) -> torch.Tensor:
+    if x.shape[0] == rows:
+        return x
+    out = torch.zeros((rows,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    out[:x.shape[0]] = x
+    return out
 
 
 def build_model(preset: str | LlamaConfig = "tiny", device="cpu", tp: TPContext | None = None, seed: int = 0,

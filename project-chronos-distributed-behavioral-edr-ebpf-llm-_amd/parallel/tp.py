@@ -64,6 +64,23 @@ class TPContext:
         self.ipc_allreduce = ar
         return ar
 
+    def reduce_scatter_rows(self, x: torch.Tensor) -> torch.Tensor:
+        """Sequence parallelism: sum over ranks of x [R * world, ...], this rank keeping rows [rank * R, (rank + 1) * R)
+        (RCCL reduce-scatter: the same bytes on the wire as half an all-reduce)."""
+        if self.world == 1:
+            return x
+        out = torch.empty((x.shape[0] // self.world,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        dist.reduce_scatter_tensor(out, x.contiguous(), group=self.group)
+        return out
+
+    def all_gather_rows(self, x: torch.Tensor) -> torch.Tensor:
+        """Sequence parallelism: [R, ...] row shards -> [R * world, ...] in rank order."""
+        if self.world == 1:
+            return x
+        out = torch.empty((x.shape[0] * self.world,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        dist.all_gather_into_tensor(out, x.contiguous(), group=self.group)
+        return out
+
     def all_gather_last(self, x: torch.Tensor) -> torch.Tensor:
         """[.., n] shards -> [.., n * world] (vocab-parallel logits)."""
         if self.world == 1:

@@ -34,9 +34,9 @@ def _run(extra):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("tp", [1, 2])
-def test_bench_two_ranks(tp):
-    r = _run(["--tp", str(tp)] if tp > 1 else [])
+@pytest.mark.parametrize("tp,sp", [(1, False), (2, False), (2, True)])
+def test_bench_two_ranks(tp, sp):
+    r = _run((["--tp", str(tp)] if tp > 1 else []) + (["--sequence-parallel"] if sp else []))
     assert r["n_gpus"] == 2 and r["steps"] == 1 and r["value"] > 0
     if tp == 1:
         assert r["config"]["parallelism"] == "dp2" and r["config"]["global_batch"] == 6
