@@ -20,6 +20,11 @@ from . import grammar as G
 
 DONE = 0
 
+# process-wide cache of compiled token automata: (vocabulary fingerprint, grammar key) -> (next, dist, byte DFA).
+# Engines in one process (DP replicas on one host, tests) share the ~seconds-long vocab walk per grammar.
+_COMPILED: dict = {}
+_COMPILED_LOCK = threading.Lock()
+
 
 @dataclass
 class CompiledGrammar:
@@ -45,6 +50,8 @@ class GrammarBank:
         self._host_dist: list[int] = [0]
         self._by_key: dict[str, CompiledGrammar] = {}
         self._lock = threading.Lock()
+        sample = b"\x00".join(token_bytes[:: max(1, len(token_bytes) // 4096)])
+        self._fp = (vocab, len(token_bytes), self.stop_ids, max_string, json_depth, max_ws, hash(sample))
         self._free_start = self._add_free()
 
     # ---- registration -------------------------------------------------------------------------------------------
@@ -81,14 +88,21 @@ class GrammarBank:
         with self._lock:
             if key in self._by_key:
                 return self._by_key[key]
-            node = G.grammar_for_format(fmt, self.json_depth, self.max_ws, self.max_string)
-            dfa = G.compile_dfa(node)
-            from ...native import constrain_lib
+            with _COMPILED_LOCK:
+                hit = _COMPILED.get((self._fp, key))
+            if hit is None:
+                node = G.grammar_for_format(fmt, self.json_depth, self.max_ws, self.max_string)
+                dfa = G.compile_dfa(node)
+                from ...native import constrain_lib
 
-            lib = constrain_lib()
-            toks = list(self.token_bytes[: self.vocab]) + [b""] * max(0, self.vocab - len(self.token_bytes))
-            nxt, dist, _live = lib.compile_token_dfa(dfa.trans, dfa.accept, toks, list(self.stop_ids), dfa.start)
-            cg = CompiledGrammar(key, self._append(np.asarray(nxt), np.asarray(dist)), dfa.num_states, dfa)
+                lib = constrain_lib()
+                toks = list(self.token_bytes[: self.vocab]) + [b""] * max(0, self.vocab - len(self.token_bytes))
+                nxt, dist, _live = lib.compile_token_dfa(dfa.trans, dfa.accept, toks, list(self.stop_ids), dfa.start)
+                hit = (np.asarray(nxt), np.asarray(dist), dfa)
+                with _COMPILED_LOCK:
+                    _COMPILED[(self._fp, key)] = hit
+            nxt, dist, dfa = hit
+            cg = CompiledGrammar(key, self._append(nxt, dist), dfa.num_states, dfa)
             self._by_key[key] = cg
             return cg
 

@@ -77,6 +77,9 @@ class EngineConfig:
     tp_sequence_parallel: bool = False  # TP prefill: reduce-scatter / all-gather around the norms instead of all-reduce
     decode_gate: bool = True       # small buckets: kernels of steps after the last live row finished return at once
     cp_min_tokens: int = 4096      # context parallel (Engine(cp=...)): prefill chunks at least this long are split
+    # token automata compiled at start-up (a first request must not pay the ~4 s vocab walk: the reference's cold-start
+    # timeout): "verdict" = the CHRONOS verdict schema the sensor sends, "json" = format:"json"
+    warm_formats: tuple = ("verdict", "json")
 
 
 @dataclass
@@ -162,6 +165,12 @@ class Engine:
         mc = self.model.cfg
         self.bank = GrammarBank(self.tok.token_bytes_list(), self.tok.stop_ids, mc.vocab_size, cfg.grammar_capacity,
                                 self.device, max_string=cfg.max_string)
+        for f in cfg.warm_formats:
+            if f == "verdict":
+                from ...sensor.prompt import VERDICT_SCHEMA
+
+                f = VERDICT_SCHEMA
+            self.bank.get(f)
         # ---- KV sizing ----
         bs = cfg.block_size
         self.max_blocks_per_seq = (cfg.max_model_len + bs - 1) // bs

@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--num-predict", type=int, default=64)
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--cp", type=int, default=1, help="context-parallel ranks (torch.distributed.run)")
+    ap.add_argument("--repeat", type=int, default=1, help="run the long request this many times (first = cold)")
     a = ap.parse_args()
     from chronos.brain.engine.engine import Engine, EngineConfig
     from chronos.parallel.tp import TPContext
@@ -74,28 +75,32 @@ def main():
     ids = eng.tok.chat_ids(build_prompt(hist[:lo]))
     print(f"[long] prompt {len(ids)} tokens, {lo} events", file=sys.stderr, flush=True)
     sync = torch.cuda.synchronize if a.device == "cuda" else (lambda: None)
-    sync()
-    t0 = time.perf_counter()
-    req = eng.submit(ids, fmt=VERDICT_SCHEMA, num_predict=a.num_predict)
-    while not req.t_first:
-        eng.step()
-        print(f"[long] prefilled {req.prefilled}/{len(ids)} at {time.perf_counter() - t0:.1f}s", file=sys.stderr,
-              flush=True)
-    sync()
-    ttft = time.perf_counter() - t0
-    eng.run_until_idle()
-    sync()
-    total = time.perf_counter() - t0
-    v = json.loads(req.text)
-    kv_bytes = eng.kv.buf.numel() * eng.kv.buf.element_size()
-    if cp is not None and cp.rank != 0:
-        return
-    print(json.dumps({
-        "config": "128k-token kill-chain context", "model": a.model, "kv_dtype": a.kv_dtype, "cp": a.cp,
-        "prompt_tokens": len(ids), "ttft_s": round(ttft, 3), "prefill_tokens_per_s": round(len(ids) / ttft, 1),
-        "verdict_tokens": len(req.out_ids), "decode_ms_per_token": round(1000 * (total - ttft) / max(1, len(req.out_ids)), 2),
-        "kv_cache_gib": round(kv_bytes / 2**30, 2), "verdict_keys": sorted(v),
-    }), flush=True)
+    for rep in range(a.repeat):
+        sync()
+        t0 = time.perf_counter()
+        req = eng.submit(ids, fmt=VERDICT_SCHEMA, num_predict=a.num_predict)
+        while not req.t_first and not req.done_reason:
+            eng.step()
+            print(f"[long] prefilled {req.prefilled}/{len(ids)} at {time.perf_counter() - t0:.1f}s", file=sys.stderr,
+                  flush=True)
+        if req.error:
+            raise SystemExit(f"request failed: {req.error}")
+        sync()
+        ttft = time.perf_counter() - t0
+        eng.run_until_idle()
+        sync()
+        total = time.perf_counter() - t0
+        v = json.loads(req.text)
+        kv_bytes = eng.kv.buf.numel() * eng.kv.buf.element_size()
+        if cp is not None and cp.rank != 0:
+            continue
+        print(json.dumps({
+            "config": "128k-token kill-chain context", "model": a.model, "kv_dtype": a.kv_dtype, "cp": a.cp,
+            "run": rep, "prompt_tokens": len(ids), "ttft_s": round(ttft, 3),
+            "prefill_tokens_per_s": round(len(ids) / ttft, 1), "verdict_tokens": len(req.out_ids),
+            "decode_ms_per_token": round(1000 * (total - ttft) / max(1, len(req.out_ids)), 2),
+            "kv_cache_gib": round(kv_bytes / 2**30, 2), "verdict_keys": sorted(v),
+        }), flush=True)
 
 
 if __name__ == "__main__":
