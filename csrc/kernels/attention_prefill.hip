@@ -22,7 +22,10 @@ constexpr int kVPitch = 80;     // V^T row pitch (bytes)
 constexpr int kVImg = 128 * kVPitch;
 constexpr int kStage = kKImg + kVImg;
 
-template <bool FP8>
+// SUB = 32-token K/V sub-tiles staged per barrier (1: the original 32-token step; 2: 64 tokens per stage, so every
+// barrier / prefetch round trip carries twice the MFMA work — the kernel is bound by the K/V load latency with one
+// stage of lookahead, profiles/r1s4_prefill_attn.jsonl).
+template <bool FP8, int SUB>
 __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(
     const uint16_t* __restrict__ q, const void* __restrict__ kcv, const void* __restrict__ vcv,
     const int32_t* __restrict__ block_table, int bt_stride, const int32_t* __restrict__ q_start,
@@ -61,55 +64,62 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(
     int last_tr = rel0 + 128 / G - 1;
     if (last_tr > qlen - 1) last_tr = qlen - 1;
     const int kv_end = ctx0 + last_tr + 1;
-    const int nsteps = (kv_end + 31) >> 5;
+    const int nsub = (kv_end + 31) >> 5;          // 32-token sub-tiles
+    const int nsteps = (nsub + SUB - 1) / SUB;    // stages (one barrier each)
     // first position any row of this wave can have (rows are token-major): keys below it need no causal mask
     const int wave_min_pos = ctx0 + rel0 + (w * 32) / G;
 
     // ---- staging assignment ----
     const int krow = threadIdx.x >> 3, kunit = (threadIdx.x & 7) * 2;     // K: 32 rows x 16 units of 16 B
     const int vrow = threadIdx.x >> 1, vhalf = threadIdx.x & 1;           // V^T: 128 rows x 2 halves of 32 B
-    u16x8 ks[2], vs[2];
+    u16x8 ks[SUB][2], vs[SUB][2];
     auto gload = [&](int s) {
-        const int tok = s * 32 + krow;
-        if (tok < kv_end) {
-            const int64_t blk = bt[tok / block_size];
-            const int64_t e = (((blk * hkv + h) * block_size) + tok % block_size) * kPD + kunit * 8;
-            if constexpr (FP8) {  // 16 fp8 -> 16 bf16 during staging: the LDS image and the math stay bf16
-                const uint4 v = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(kcv) + e);
-                ks[0] = __builtin_bit_cast(u16x8, fp8x8_to_bf16x8(v.x, v.y, k_scale));
-                ks[1] = __builtin_bit_cast(u16x8, fp8x8_to_bf16x8(v.z, v.w, k_scale));
+#pragma unroll
+        for (int j = 0; j < SUB; ++j) {
+            const int tok = (s * SUB + j) * 32 + krow;
+            if (tok < kv_end) {
+                const int64_t blk = bt[tok / block_size];
+                const int64_t e = (((blk * hkv + h) * block_size) + tok % block_size) * kPD + kunit * 8;
+                if constexpr (FP8) {  // 16 fp8 -> 16 bf16 during staging: the LDS image and the math stay bf16
+                    const uint4 v = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(kcv) + e);
+                    ks[j][0] = __builtin_bit_cast(u16x8, fp8x8_to_bf16x8(v.x, v.y, k_scale));
+                    ks[j][1] = __builtin_bit_cast(u16x8, fp8x8_to_bf16x8(v.z, v.w, k_scale));
+                } else {
+                    const u16x8* p = reinterpret_cast<const u16x8*>(kc + e);
+                    ks[j][0] = p[0];
+                    ks[j][1] = p[1];
+                }
             } else {
-                const u16x8* p = reinterpret_cast<const u16x8*>(kc + e);
-                ks[0] = p[0];
-                ks[1] = p[1];
+                ks[j][0] = ks[j][1] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
             }
-        } else {
-            ks[0] = ks[1] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
-        }
-        const int vt = s * 32 + vhalf * 16;
-        if (vt < kv_end) {
-            const int64_t blk = bt[vt / block_size];
-            const int64_t e = ((blk * hkv + h) * kPD + vrow) * (int64_t)block_size + vt % block_size;
-            if constexpr (FP8) {
-                const uint4 v = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(vcv) + e);
-                vs[0] = __builtin_bit_cast(u16x8, fp8x8_to_bf16x8(v.x, v.y, v_scale));
-                vs[1] = __builtin_bit_cast(u16x8, fp8x8_to_bf16x8(v.z, v.w, v_scale));
+            const int vt = (s * SUB + j) * 32 + vhalf * 16;
+            if (vt < kv_end) {
+                const int64_t blk = bt[vt / block_size];
+                const int64_t e = ((blk * hkv + h) * kPD + vrow) * (int64_t)block_size + vt % block_size;
+                if constexpr (FP8) {
+                    const uint4 v = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(vcv) + e);
+                    vs[j][0] = __builtin_bit_cast(u16x8, fp8x8_to_bf16x8(v.x, v.y, v_scale));
+                    vs[j][1] = __builtin_bit_cast(u16x8, fp8x8_to_bf16x8(v.z, v.w, v_scale));
+                } else {
+                    const u16x8* p = reinterpret_cast<const u16x8*>(vc + e);
+                    vs[j][0] = p[0];
+                    vs[j][1] = p[1];
+                }
             } else {
-                const u16x8* p = reinterpret_cast<const u16x8*>(vc + e);
-                vs[0] = p[0];
-                vs[1] = p[1];
+                vs[j][0] = vs[j][1] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
             }
-        } else {
-            vs[0] = vs[1] = u16x8{0, 0, 0, 0, 0, 0, 0, 0};
         }
     };
     auto swrite = [&](int buf) {
-        unsigned char* base = lds + buf * kStage;
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int u = (kunit + j) ^ (krow & 15);
-            *reinterpret_cast<u16x8*>(base + krow * 256 + u * 16) = ks[j];
-            *reinterpret_cast<u16x8*>(base + kKImg + vrow * kVPitch + vhalf * 32 + j * 16) = vs[j];
+        for (int j = 0; j < SUB; ++j) {
+            unsigned char* base = lds + (buf * SUB + j) * kStage;
+#pragma unroll
+            for (int jj = 0; jj < 2; ++jj) {
+                const int u = (kunit + jj) ^ (krow & 15);
+                *reinterpret_cast<u16x8*>(base + krow * 256 + u * 16) = ks[j][jj];
+                *reinterpret_cast<u16x8*>(base + kKImg + vrow * kVPitch + vhalf * 32 + jj * 16) = vs[j][jj];
+            }
         }
     };
 
@@ -126,74 +136,80 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(
     }
     __syncthreads();
     for (int s = 0; s < nsteps; ++s) {
-        if (s + 1 < nsteps) gload(s + 1);  // in flight under this step's MFMAs
-        const unsigned char* base = lds + (s & 1) * kStage;
-        const int t0 = s * 32;
-        // K fragments, shared by both m-tiles
-        bf16x8 kf[2][4];
+        if (s + 1 < nsteps) gload(s + 1);  // in flight under this stage's MFMAs
 #pragma unroll
-        for (int g = 0; g < 2; ++g) {
-            const int row = g * 16 + r;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                const int u = (4 * c + h4) ^ (row & 15);
-                kf[g][c] = *reinterpret_cast<const bf16x8*>(base + row * 256 + u * 16);
-            }
-        }
-        bf16x8 vf[8];
-#pragma unroll
-        for (int dt = 0; dt < 8; ++dt) {
-            const unsigned char* vr = base + kKImg + (dt * 16 + r) * kVPitch;
-            const bf16x4 a = *reinterpret_cast<const bf16x4*>(vr + 8 * h4);
-            const bf16x4 b = *reinterpret_cast<const bf16x4*>(vr + 32 + 8 * h4);
-            vf[dt] = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
-        }
-        const bool edge = (t0 + 32 > kv_end) || (t0 + 31 > wave_min_pos);
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-            f32x4 sc[2];
+        for (int j = 0; j < SUB; ++j) {
+            const int sub = s * SUB + j;
+            if (sub < nsub) {  // uniform
+            const unsigned char* base = lds + ((s & 1) * SUB + j) * kStage;
+            const int t0 = sub * 32;
+            // K fragments, shared by both m-tiles
+            bf16x8 kf[2][4];
 #pragma unroll
             for (int g = 0; g < 2; ++g) {
-                f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+                const int row = g * 16 + r;
 #pragma unroll
-                for (int c = 0; c < 4; ++c) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[g][c], qf[mt][c], acc, 0, 0, 0);
-                sc[g] = acc;
+                for (int c = 0; c < 4; ++c) {
+                    const int u = (4 * c + h4) ^ (row & 15);
+                    kf[g][c] = *reinterpret_cast<const bf16x8*>(base + row * 256 + u * 16);
+                }
             }
-            float mx = -INFINITY;
-#pragma unroll
-            for (int g = 0; g < 2; ++g)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    float v = sc[g][i] * scale_log2;
-                    if (edge) {
-                        const int tok = t0 + 16 * g + 4 * h4 + i;
-                        if (tok >= kv_end || tok > rpos[mt]) v = -INFINITY;
-                    } else if (rpos[mt] < 0) {
-                        v = -INFINITY;
-                    }
-                    sc[g][i] = v;
-                    mx = fmaxf(mx, v);
-                }
-            mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-            const float mnew = fmaxf(m[mt], mx);
-            const float alpha = exp2f(m[mt] - mnew);
-            m[mt] = mnew;
-            float ps = 0.f;
-            bf16x8 pf;
-#pragma unroll
-            for (int g = 0; g < 2; ++g)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    const float p = exp2f(sc[g][i] - mnew);
-                    ps += p;
-                    pf[4 * g + i] = (__bf16)p;
-                }
-            lsum[mt] = lsum[mt] * alpha + ps;
+            bf16x8 vf[8];
 #pragma unroll
             for (int dt = 0; dt < 8; ++dt) {
-                o[mt][dt] *= alpha;
-                o[mt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[dt], pf, o[mt][dt], 0, 0, 0);
+                const unsigned char* vr = base + kKImg + (dt * 16 + r) * kVPitch;
+                const bf16x4 a = *reinterpret_cast<const bf16x4*>(vr + 8 * h4);
+                const bf16x4 b = *reinterpret_cast<const bf16x4*>(vr + 32 + 8 * h4);
+                vf[dt] = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+            }
+            const bool edge = (t0 + 32 > kv_end) || (t0 + 31 > wave_min_pos);
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                f32x4 sc[2];
+#pragma unroll
+                for (int g = 0; g < 2; ++g) {
+                    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[g][c], qf[mt][c], acc, 0, 0, 0);
+                    sc[g] = acc;
+                }
+                float mx = -INFINITY;
+#pragma unroll
+                for (int g = 0; g < 2; ++g)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        float v = sc[g][i] * scale_log2;
+                        if (edge) {
+                            const int tok = t0 + 16 * g + 4 * h4 + i;
+                            if (tok >= kv_end || tok > rpos[mt]) v = -INFINITY;
+                        } else if (rpos[mt] < 0) {
+                            v = -INFINITY;
+                        }
+                        sc[g][i] = v;
+                        mx = fmaxf(mx, v);
+                    }
+                mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+                mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+                const float mnew = fmaxf(m[mt], mx);
+                const float alpha = exp2f(m[mt] - mnew);
+                m[mt] = mnew;
+                float ps = 0.f;
+                bf16x8 pf;
+#pragma unroll
+                for (int g = 0; g < 2; ++g)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const float p = exp2f(sc[g][i] - mnew);
+                        ps += p;
+                        pf[4 * g + i] = (__bf16)p;
+                    }
+                lsum[mt] = lsum[mt] * alpha + ps;
+#pragma unroll
+                for (int dt = 0; dt < 8; ++dt) {
+                    o[mt][dt] *= alpha;
+                    o[mt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[dt], pf, o[mt][dt], 0, 0, 0);
+                }
+            }
             }
         }
         if (s + 1 < nsteps) swrite((s + 1) & 1);
@@ -221,27 +237,284 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(
     }
 }
 
+// ------------------------------------------------------------------------------------------------------------------
+// v2: 32x32x16 MFMAs with the score tile reused in registers as the P·V operand (cdna_hip_programming.md §3 "An
+// accumulator tile as the next MFMA's operand").  Per wave 32 query rows, 64 keys per stage:
+//   S^T[key, row] = K[key, :] . Q[row, :]   — mfma_32x32x16(A = K rows from LDS, B = Q^T in registers), 2 key blocks;
+//     a lane owns ONE query row (col = lane & 31) and 32 of the stage's 64 keys (rows (r&3)+8(r>>2)+4h of each block),
+//     so the row max is 31 in-lane fmax + one exchange with the partner lane (lane ^ 32) — no 16-lane shuffles;
+//   O^T[dim, row] += V^T[dim, key] . P^T[key, row] — the exp'd scores converted pairwise to bf16 ARE the B operand
+//     (registers 8s..8s+7 = k-step s); the V^T fragment is read in the same permuted key order (two 8-byte reads).
+// LDS per stage: K [64 keys][256 B] with the 16-B unit XOR-swizzled by (key & 15) (conflict-free ds_read_b128 of the
+// A fragments); V^T [128 dims][64 keys] with a 136-B row pitch (34 dwords: the 32 lanes of an 8-byte read cover all
+// 64 banks).  Register-staged K/V for stage s+1 are in flight under stage s, one barrier per stage.
+// ------------------------------------------------------------------------------------------------------------------
+constexpr int kK2Img = 64 * 256;        // K image bytes per stage
+constexpr int kV2Pitch = 136;           // V^T row pitch (bytes)
+constexpr int kV2Img = 128 * kV2Pitch;  // V^T image bytes per stage
+constexpr int kStage2 = kK2Img + kV2Img;
+
+template <bool FP8>
+__global__ void __launch_bounds__(256, 2) attn_prefill2_kernel(
+    const uint16_t* __restrict__ q, const void* __restrict__ kcv, const void* __restrict__ vcv,
+    const int32_t* __restrict__ block_table, int bt_stride, const int32_t* __restrict__ q_start,
+    const int32_t* __restrict__ ctx_len, const int32_t* __restrict__ tiles, int ntiles, uint16_t* __restrict__ out,
+    int hq, int hkv, int block_size, float scale_log2, float k_scale, float v_scale) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    typedef float f32x16_t __attribute__((ext_vector_type(16)));
+    const uint16_t* kc = reinterpret_cast<const uint16_t*>(kcv);
+    const uint16_t* vc = reinterpret_cast<const uint16_t*>(vcv);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int col = lane & 31, hf = lane >> 5;
+    const int G = hq / hkv;
+    const int h = blockIdx.y;
+    const int tile = ntiles - 1 - (int)blockIdx.x;  // heaviest first
+    const int seq = tiles[2 * tile], rel0 = tiles[2 * tile + 1];
+    const int qbase = q_start[seq], qlen = q_start[seq + 1] - qbase;
+    const int ctx = ctx_len[seq], ctx0 = ctx - qlen;
+    const int32_t* bt = block_table + (int64_t)seq * bt_stride;
+
+    // ---- this lane's query row: Q^T fragments (B operand: k = dims 16c + 8hf + j, col = row) ----
+    const int R = w * 32 + col;
+    const int tr = rel0 + R / G, hd = h * G + R % G;
+    const bool rvalid = tr < qlen;
+    const int rpos = rvalid ? ctx0 + tr : -1;
+    bf16x8 qf[8];
+    {
+        const uint16_t* qp = q + ((int64_t)(qbase + (rvalid ? tr : 0)) * hq + hd) * kPD + 8 * hf;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            bf16x8 v = *reinterpret_cast<const bf16x8*>(qp + 16 * c);
+            if (!rvalid) v = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+            qf[c] = v;
+        }
+    }
+    int last_tr = rel0 + 128 / G - 1;
+    if (last_tr > qlen - 1) last_tr = qlen - 1;
+    const int kv_end = ctx0 + last_tr + 1;
+    const int nsteps = (kv_end + 63) >> 6;
+    const int wave_min_pos = ctx0 + rel0 + (w * 32) / G;  // keys below it need no causal mask for this wave
+
+    // ---- staging: K 64 keys x 4 x 16 B per thread-quarter; V^T 128 dims x 2 halves of 32 keys ----
+    const int kkey = threadIdx.x >> 2, kq = threadIdx.x & 3;
+    const int vdim = threadIdx.x >> 1, vh = threadIdx.x & 1;
+    u16x8 ks[4], vs[4];
+    // Out-of-range keys load from the sequence's first page (always mapped) and are zeroed by a mask: no branch
+    // around the loads, so the compiler keeps the staging registers (a branch made it merge them through scratch
+    // and wait for the loads right away) and the tile stays in flight under the MFMAs.  Zeroed V keeps stale cache
+    // bytes (possibly NaN) out of O even though their P is 0.
+    auto gload = [&](int s) {
+        const int tok = s * 64 + kkey;
+        const bool kval = tok < kv_end;
+        const int tk = kval ? tok : 0;
+        const uint16_t km = kval ? 0xFFFF : 0;
+        {
+            const int64_t blk = bt[tk / block_size];
+            const int64_t e = (((blk * hkv + h) * block_size) + tk % block_size) * kPD + kq * 32;
+            if constexpr (FP8) {
+                const uint4* p = reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(kcv) + e);
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    const uint4 v = p[j];
+                    ks[2 * j] = __builtin_bit_cast(u16x8, fp8x8_to_bf16x8(v.x, v.y, k_scale));
+                    ks[2 * j + 1] = __builtin_bit_cast(u16x8, fp8x8_to_bf16x8(v.z, v.w, k_scale));
+                }
+            } else {
+                const u16x8* p = reinterpret_cast<const u16x8*>(kc + e);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) ks[j] = p[j];
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) ks[j] &= km;
+        }
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {  // two 16-token pages of this thread's 32-key half
+            const int vt = s * 64 + vh * 32 + b * 16;
+            const bool vval = vt < kv_end;
+            const int tv = vval ? vt : 0;
+            const uint16_t vm = vval ? 0xFFFF : 0;
+            const int64_t blk = bt[tv / block_size];
+            const int64_t e = ((blk * hkv + h) * kPD + vdim) * (int64_t)block_size + tv % block_size;
+            if constexpr (FP8) {
+                const uint4 v = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(vcv) + e);
+                vs[2 * b] = __builtin_bit_cast(u16x8, fp8x8_to_bf16x8(v.x, v.y, v_scale));
+                vs[2 * b + 1] = __builtin_bit_cast(u16x8, fp8x8_to_bf16x8(v.z, v.w, v_scale));
+            } else {
+                const u16x8* p = reinterpret_cast<const u16x8*>(vc + e);
+                vs[2 * b] = p[0];
+                vs[2 * b + 1] = p[1];
+            }
+            vs[2 * b] &= vm;
+            vs[2 * b + 1] &= vm;
+        }
+    };
+    auto swrite = [&](int buf) {
+        unsigned char* base = lds + buf * kStage2;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int u = (kq * 4 + j) ^ (kkey & 15);
+            *reinterpret_cast<u16x8*>(base + kkey * 256 + u * 16) = ks[j];
+        }
+        unsigned char* vr = base + kK2Img + vdim * kV2Pitch + vh * 64;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {  // 8-byte stores: the 136-B pitch keeps rows 8-B aligned only
+            const u16x8 v = vs[j];
+            *reinterpret_cast<u16x4*>(vr + 16 * j) = u16x4{v[0], v[1], v[2], v[3]};
+            *reinterpret_cast<u16x4*>(vr + 16 * j + 8) = u16x4{v[4], v[5], v[6], v[7]};
+        }
+    };
+
+    float m = -1e30f, lsum = 0.f;
+    f32x16_t o[4];
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[db][i] = 0.f;
+
+    if (nsteps > 0) {
+        gload(0);
+        swrite(0);
+    }
+    __syncthreads();
+    for (int s = 0; s < nsteps; ++s) {
+        if (s + 1 < nsteps) gload(s + 1);  // in flight under this stage's MFMAs
+        const unsigned char* base = lds + (s & 1) * kStage2;
+        const int t0 = s * 64;
+        // ---- S^T for the stage's two 32-key blocks ----
+        f32x16_t sc[2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            f32x16_t acc;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+            const int row = kb * 32 + col;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const int u = (2 * c + hf) ^ (row & 15);
+                const bf16x8 kf = *reinterpret_cast<const bf16x8*>(base + row * 256 + u * 16);
+                acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[c], acc, 0, 0, 0);
+            }
+            sc[kb] = acc;
+        }
+        // ---- online softmax over this lane's 32 keys + the partner lane's 32 ----
+        const bool edge = (t0 + 64 > kv_end) || (t0 + 63 > wave_min_pos);
+        float mx = -INFINITY;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                float v = sc[kb][i] * scale_log2;
+                if (edge) {
+                    const int tok = t0 + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * hf;
+                    if (tok >= kv_end || tok > rpos) v = -INFINITY;
+                } else if (rpos < 0) {
+                    v = -INFINITY;
+                }
+                sc[kb][i] = v;
+                mx = fmaxf(mx, v);
+            }
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float mnew = fmaxf(m, mx);
+        const float alpha = exp2f(m - mnew);
+        m = mnew;
+        float ps = 0.f;
+        bf16x8 pf[2][2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const float p = exp2f(sc[kb][i] - mnew);
+                ps += p;
+                pf[kb][i >> 3][i & 7] = (__bf16)p;
+            }
+        lsum = lsum * alpha + ps;
+#pragma unroll
+        for (int db = 0; db < 4; ++db) o[db] *= alpha;
+        // ---- O^T += V^T . P^T (k-step (kb, s2): keys kb*32 + 16 s2 + 8 (j>>2) + 4 hf + (j&3)) ----
+#pragma unroll
+        for (int db = 0; db < 4; ++db) {
+            const unsigned char* vr = base + kK2Img + (db * 32 + col) * kV2Pitch;
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    const int k0 = kb * 32 + 16 * s2 + 4 * hf;
+                    const bf16x4 a = *reinterpret_cast<const bf16x4*>(vr + 2 * k0);
+                    const bf16x4 b = *reinterpret_cast<const bf16x4*>(vr + 2 * (k0 + 8));
+                    const bf16x8 vf = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+                    o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kb][s2], o[db], 0, 0, 0);
+                }
+        }
+        if (s + 1 < nsteps) swrite((s + 1) & 1);
+        __syncthreads();
+    }
+
+    // ---- epilogue: lane holds O^T[dims 32 db + 8 g + 4 hf + (0..3)][its row] ----
+    const float lt = lsum + __shfl_xor(lsum, 32, 64);
+    if (!rvalid) return;
+    const float inv = lt > 0.f ? 1.f / lt : 0.f;
+    uint16_t* op = out + ((int64_t)(qbase + tr) * hq + hd) * kPD + 4 * hf;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            u16x4 v;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = f2bf(o[db][4 * g + i] * inv);
+            *reinterpret_cast<u16x4*>(op + 32 * db + 8 * g) = v;
+        }
+}
+
 void launch_attn_prefill(const uint16_t* q, const void* kc, const void* vc, const int32_t* block_table,
                          int bt_stride, const int32_t* q_start, const int32_t* ctx_len, const int32_t* tiles,
                          int ntiles, uint16_t* out, int hq, int hkv, int block_size, float scale, bool fp8,
                          float k_scale, float v_scale, hipStream_t st) {
     if (ntiles == 0) return;
+    const int variant = knob("prefill_variant", 2);
+    if (variant == 2) {
+        static bool attr2 = [] {
+            return hipFuncSetAttribute((const void*)attn_prefill2_kernel<false>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kStage2) == hipSuccess &&
+                   hipFuncSetAttribute((const void*)attn_prefill2_kernel<true>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kStage2) == hipSuccess;
+        }();
+        (void)attr2;
+        const float sl2 = scale * 1.4426950408889634f;
+        if (fp8)
+            hipLaunchKernelGGL(attn_prefill2_kernel<true>, dim3(ntiles, hkv), dim3(256), 2 * kStage2, st, q, kc, vc,
+                               block_table, bt_stride, q_start, ctx_len, tiles, ntiles, out, hq, hkv, block_size, sl2,
+                               k_scale, v_scale);
+        else
+            hipLaunchKernelGGL(attn_prefill2_kernel<false>, dim3(ntiles, hkv), dim3(256), 2 * kStage2, st, q, kc, vc,
+                               block_table, bt_stride, q_start, ctx_len, tiles, ntiles, out, hq, hkv, block_size, sl2,
+                               1.f, 1.f);
+        return;
+    }
+    const int sub = variant == 1 ? 2 : 1;
     static bool attr = [] {
-        return hipFuncSetAttribute((const void*)attn_prefill_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   2 * kStage) == hipSuccess &&
-               hipFuncSetAttribute((const void*)attn_prefill_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   2 * kStage) == hipSuccess;
+        bool ok = true;
+        ok &= hipFuncSetAttribute((const void*)attn_prefill_kernel<false, 1>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kStage) == hipSuccess;
+        ok &= hipFuncSetAttribute((const void*)attn_prefill_kernel<true, 1>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kStage) == hipSuccess;
+        ok &= hipFuncSetAttribute((const void*)attn_prefill_kernel<false, 2>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kStage) == hipSuccess;
+        ok &= hipFuncSetAttribute((const void*)attn_prefill_kernel<true, 2>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kStage) == hipSuccess;
+        return ok;
     }();
     (void)attr;
     const float sl = scale * 1.4426950408889634f;
-    if (fp8)
-        hipLaunchKernelGGL(attn_prefill_kernel<true>, dim3(ntiles, hkv), dim3(256), 2 * kStage, st, q, kc, vc,
-                           block_table, bt_stride, q_start, ctx_len, tiles, ntiles, out, hq, hkv, block_size, sl,
-                           k_scale, v_scale);
-    else
-        hipLaunchKernelGGL(attn_prefill_kernel<false>, dim3(ntiles, hkv), dim3(256), 2 * kStage, st, q, kc, vc,
-                           block_table, bt_stride, q_start, ctx_len, tiles, ntiles, out, hq, hkv, block_size, sl,
-                           1.f, 1.f);
+    const size_t lds = (size_t)2 * sub * kStage;
+#define AP_LAUNCH(F, S, KS, VS)                                                                                    \
+    hipLaunchKernelGGL((attn_prefill_kernel<F, S>), dim3(ntiles, hkv), dim3(256), lds, st, q, kc, vc, block_table, \
+                       bt_stride, q_start, ctx_len, tiles, ntiles, out, hq, hkv, block_size, sl, KS, VS)
+    if (fp8) {
+        if (sub == 2) AP_LAUNCH(true, 2, k_scale, v_scale); else AP_LAUNCH(true, 1, k_scale, v_scale);
+    } else {
+        if (sub == 2) AP_LAUNCH(false, 2, 1.f, 1.f); else AP_LAUNCH(false, 1, 1.f, 1.f);
+    }
+#undef AP_LAUNCH
 }
 
 }  // namespace chronos

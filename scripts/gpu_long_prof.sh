@@ -7,10 +7,10 @@ export TMPDIR=/tmp
 mkdir -p gpurun_out
 TOK=${TOK:-131000}
 PTOK=${PTOK:-49152}
-CHRONOS_PHASE_SYNC=1 timeout -k 10 400 python3 scripts/long_context.py --tokens $TOK > gpurun_out/long.log 2>&1 || exit $?
-grep prefilled gpurun_out/long.log | tail -9; tail -1 gpurun_out/long.log
+CHRONOS_PHASE_SYNC=1 timeout -k 10 400 python3 scripts/long_context.py --tokens $TOK --repeat 2 > gpurun_out/long.log 2>&1 || exit $?
+grep prefilled gpurun_out/long.log | tail -8; grep "^{" gpurun_out/long.log
 timeout -k 10 500 rocprofv3 --kernel-trace --stats -d /tmp/lprof -o long --output-format csv -- \
-    python3 scripts/long_context.py --tokens $PTOK --num-predict 8 > gpurun_out/long_prof.log 2>&1 || exit $?
+    python3 scripts/long_context.py --tokens $PTOK --num-predict 32 > gpurun_out/long_prof.log 2>&1 || exit $?
 mkdir -p gpurun_out/lprof && cp $(find /tmp/lprof -name "*kernel_stats.csv") gpurun_out/lprof/
 python3 - <<'PY'
 import csv, glob
