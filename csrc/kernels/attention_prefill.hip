@@ -246,11 +246,13 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(
 //   O^T[dim, row] += V^T[dim, key] . P^T[key, row] — the exp'd scores converted pairwise to bf16 ARE the B operand
 //     (registers 8s..8s+7 = k-step s); the V^T fragment is read in the same permuted key order (two 8-byte reads).
 // LDS per stage: K [64 keys][256 B] with the 16-B unit XOR-swizzled by (key & 15) (conflict-free ds_read_b128 of the
-// A fragments); V^T [128 dims][64 keys] with a 136-B row pitch (34 dwords: the 32 lanes of an 8-byte read cover all
-// 64 banks).  Register-staged K/V for stage s+1 are in flight under stage s, one barrier per stage.
+// A fragments); V^T [128 dims][64 keys] with a 144-B row pitch (9 x 16 B: the 16 lanes of a ds_read_b128 group land
+// on distinct bank quads) and the keys of every 16-key group stored in the P operand's k order
+// [0-3, 8-11, 4-7, 12-15], so each V^T fragment is ONE 16-byte read.  Register-staged K/V for stage s+1 are in
+// flight under stage s, one barrier per stage.
 // ------------------------------------------------------------------------------------------------------------------
 constexpr int kK2Img = 64 * 256;        // K image bytes per stage
-constexpr int kV2Pitch = 136;           // V^T row pitch (bytes)
+constexpr int kV2Pitch = 144;           // V^T row pitch (bytes)
 constexpr int kV2Img = 128 * kV2Pitch;  // V^T image bytes per stage
 constexpr int kStage2 = kK2Img + kV2Img;
 
@@ -357,10 +359,11 @@ __global__ void __launch_bounds__(256, 2) attn_prefill2_kernel(
         }
         unsigned char* vr = base + kK2Img + vdim * kV2Pitch + vh * 64;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {  // 8-byte stores: the 136-B pitch keeps rows 8-B aligned only
+        for (int j = 0; j < 4; ++j) {  // vs[j] = keys 8j..8j+7 of this thread's 32: quads go to k-order slots
             const u16x8 v = vs[j];
-            *reinterpret_cast<u16x4*>(vr + 16 * j) = u16x4{v[0], v[1], v[2], v[3]};
-            *reinterpret_cast<u16x4*>(vr + 16 * j + 8) = u16x4{v[4], v[5], v[6], v[7]};
+            const int g16 = (j >> 1) * 32, odd = j & 1;  // byte offset of the 16-key group; upper half of it?
+            *reinterpret_cast<u16x4*>(vr + g16 + 8 * odd) = u16x4{v[0], v[1], v[2], v[3]};       // keys 8o+0..3
+            *reinterpret_cast<u16x4*>(vr + g16 + 16 + 8 * odd) = u16x4{v[4], v[5], v[6], v[7]};  // keys 8o+4..7
         }
     };
 
@@ -438,10 +441,7 @@ __global__ void __launch_bounds__(256, 2) attn_prefill2_kernel(
             for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
                 for (int s2 = 0; s2 < 2; ++s2) {
-                    const int k0 = kb * 32 + 16 * s2 + 4 * hf;
-                    const bf16x4 a = *reinterpret_cast<const bf16x4*>(vr + 2 * k0);
-                    const bf16x4 b = *reinterpret_cast<const bf16x4*>(vr + 2 * (k0 + 8));
-                    const bf16x8 vf = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+                    const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vr + 2 * (kb * 32 + 16 * s2 + 8 * hf));
                     o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kb][s2], o[db], 0, 0, 0);
                 }
         }

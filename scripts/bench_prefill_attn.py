@@ -65,6 +65,7 @@ def case(q_lens, prefix, hq=32, hkv=8, bs=16, seed=0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--variants", default="0")
+    ap.add_argument("--knob", default="prefill_variant", help="kernel knob the variants are values of")
     ap.add_argument("--out", default=None)
     ap.add_argument("--check", action="store_true", help="compare each variant with the fp32 reference (slow)")
     a = ap.parse_args()
@@ -85,7 +86,7 @@ def main():
         rec = dict(case=name, tflop=round(flops / 1e12, 2))
         base = None
         for var in variants:
-            torch.ops.chronos.set_knob("prefill_variant", var)
+            torch.ops.chronos.set_knob(a.knob, var)
             us = timeit(lambda: ops.paged_attention(*args))
             y = ops.paged_attention(*args)
             if base is None:
@@ -96,7 +97,7 @@ def main():
         if a.check and name == "wave_176x93":
             r = ref.paged_attention(*args)
             rec["maxerr_vs_fp32"] = float((base.float() - r.float()).abs().max())
-        torch.ops.chronos.set_knob("prefill_variant", variants[0])
+        torch.ops.chronos.set_knob(a.knob, variants[0])
         out.append(rec)
         print(json.dumps(rec), flush=True)
     if a.out:
