@@ -241,10 +241,14 @@ def attention_tiles(q_lens: list[int], hq: int, hkv: int, nqt: int) -> list[tupl
     return out
 
 
+_SPLIT_WGS = int(os.environ.get("CHRONOS_DECODE_SPLIT_WGS", "2"))   # target workgroups per CU
+_SPLIT_MAX = int(os.environ.get("CHRONOS_DECODE_SPLIT_MAX", "64"))
+
+
 def pick_nsplit(n_workgroups: int, max_ctx: int, cus: int = 256) -> int:
     """Flash-decoding split: enough workgroups to cover the chip, >= 256 keys per split."""
-    if n_workgroups >= 2 * cus:
+    if n_workgroups >= _SPLIT_WGS * cus:
         return 1
-    want = (2 * cus + n_workgroups - 1) // n_workgroups
+    want = (_SPLIT_WGS * cus + n_workgroups - 1) // n_workgroups
     cap = max(1, max_ctx // 256)
-    return int(max(1, min(want, cap, 64)))
+    return int(max(1, min(want, cap, _SPLIT_MAX)))
