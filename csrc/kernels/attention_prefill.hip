@@ -255,6 +255,7 @@ constexpr int kK2Img = 64 * 256;        // K image bytes per stage
 constexpr int kV2Pitch = 144;           // V^T row pitch (bytes)
 constexpr int kV2Img = 128 * kV2Pitch;  // V^T image bytes per stage
 constexpr int kStage2 = kK2Img + kV2Img;
+constexpr float kRescaleThr = 8.f;     // defer-max threshold (log2 units)
 
 template <bool FP8>
 __global__ void __launch_bounds__(256, 2) attn_prefill2_kernel(
@@ -417,22 +418,29 @@ __global__ void __launch_bounds__(256, 2) attn_prefill2_kernel(
                 mx = fmaxf(mx, v);
             }
         mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        const float mnew = fmaxf(m, mx);
-        const float alpha = exp2f(m - mnew);
-        m = mnew;
+        // defer-max (cdna_hip_programming.md T13): O and l are rescaled only when some row's max grew more than
+        // kRescaleThr (log2 units) past the max its running sums use — a wave-uniform branch, rare once the causal
+        // prefix has been seen; otherwise p = 2^(s - stale max) <= 2^kRescaleThr, exact in f32, fine as bf16.  The
+        // decision is taken before this tile's P is formed, so every P.V and l term of the tile sees one factor.
+        if (__any(mx > m + kRescaleThr)) {
+            const float mnew = fmaxf(m, mx);
+            const float alpha = exp2f(m - mnew);
+            m = mnew;
+            lsum *= alpha;
+#pragma unroll
+            for (int db = 0; db < 4; ++db) o[db] *= alpha;
+        }
         float ps = 0.f;
         bf16x8 pf[2][2];
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                const float p = exp2f(sc[kb][i] - mnew);
+                const float p = exp2f(sc[kb][i] - m);
                 ps += p;
                 pf[kb][i >> 3][i & 7] = (__bf16)p;
             }
-        lsum = lsum * alpha + ps;
-#pragma unroll
-        for (int db = 0; db < 4; ++db) o[db] *= alpha;
+        lsum += ps;
         // ---- O^T += V^T . P^T (k-step (kb, s2): keys kb*32 + 16 s2 + 8 (j>>2) + 4 hf + (j&3)) ----
 #pragma unroll
         for (int db = 0; db < 4; ++db) {

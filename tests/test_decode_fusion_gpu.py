@@ -307,3 +307,37 @@ def test_input_checks_catch_bad_indices_before_launch():
         assert r.done_reason in ("stop", "length") and r.out_ids
     finally:
         ops.set_input_checks(False)
+
+
+@pytest.mark.parametrize("variant", [0, 2])
+def test_flash_prefill_forced_rescale(variant):
+    """The flash prefill kernels' rescale paths, forced: late keys whose scores jump far past the running max (v2's
+    deferred-max branch, cdna_hip_programming.md §5.4 rule 26) and a spike against one query row, over a 1200-token
+    chunk on a 900-token prefix; full-tensor fp32 reference."""
+    from chronos import ops
+    from chronos.ops import reference as ref
+
+    torch.ops.chronos.set_knob("prefill_variant", variant)
+    try:
+        g = torch.Generator(device=DEV).manual_seed(123 + variant)
+        hq, hkv, bs = 32, 8, 16
+        q_lens, prefix = [1200], [900]
+        ctx = [p + n for p, n in zip(prefix, q_lens)]
+        nb = (ctx[0] + bs - 1) // bs + 1
+        k = (torch.randn(nb, hkv, bs, 128, device=DEV, generator=g) * 0.3).to(torch.bfloat16)
+        v = torch.randn(nb, hkv, 128, bs, device=DEV, generator=g).to(torch.bfloat16)
+        bt = torch.arange(1, nb, dtype=torch.int32, device=DEV).view(1, -1)
+        q = torch.randn(q_lens[0], hq, 128, device=DEV, generator=g).to(torch.bfloat16)
+        # keys 1500..1563 (stage 23) of kv head 3 aligned with q rows: their scores jump ~+40 (log2) past the max
+        for t in range(1500, 1564):
+            k[1 + t // bs, 3, t % bs] = (q[t - 900, 12].float() * 0.9).to(torch.bfloat16)
+        qs = torch.tensor([0, q_lens[0]], dtype=torch.int32, device=DEV)
+        cl = torch.tensor(ctx, dtype=torch.int32, device=DEV)
+        tiles = ops.attention_tiles(q_lens, hq, hkv, 8)
+        tt = torch.tensor(tiles, dtype=torch.int32, device=DEV).view(-1, 2)
+        out = ops.paged_attention(q, k, v, bt, qs, cl, tt, len(tiles), 8, 1)
+        exp = ref.paged_attention(q, k, v, bt, qs, cl, tt, len(tiles), 8, 1)
+        d = (out.float() - exp.float()).abs()
+        assert bool((d <= 2e-2 + 2e-2 * exp.float().abs()).all()), float(d.max())
+    finally:
+        torch.ops.chronos.set_knob("prefill_variant", 2)
