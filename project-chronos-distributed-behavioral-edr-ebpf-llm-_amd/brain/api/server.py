@@ -50,7 +50,9 @@ def make_app(backend, model_name: str = "llama3", request_timeout: float | None 
             except asyncio.TimeoutError:
                 return web.json_response({"error": "generation timed out"}, status=504)
             if getattr(req, "error", None):
-                return web.json_response({"error": req.error}, status=400)
+                # a request the engine rejected is the client's fault (400); a failed engine step is ours (500)
+                internal = (getattr(req, "meta", None) or {}).get("internal_error", False)
+                return web.json_response({"error": req.error}, status=500 if internal else 400)
             return web.json_response(chat_response(model, req) if chat else generate_response(model, req))
         resp = web.StreamResponse(headers={"Content-Type": "application/x-ndjson"})
         await resp.prepare(request)

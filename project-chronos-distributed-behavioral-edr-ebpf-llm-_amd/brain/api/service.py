@@ -35,6 +35,8 @@ class EngineService:
         self._step_t0: Optional[float] = None  # start of the step in progress (None between steps)
         self.stalled = False
         self.last_error: Optional[str] = None
+        self.failures = 0
+        self.fail_backoff_s = 0.1
         self._thread = threading.Thread(target=self._loop, name="chronos-scheduler", daemon=True)
         self._watchdog = threading.Thread(target=self._watch, name="chronos-watchdog", daemon=True)
         self.started = time.time()
@@ -66,15 +68,29 @@ class EngineService:
                     with trace.range("engine.step"):
                         done = eng.step()
                 except Exception as e:  # an engine fault fails loudly in health, never silently
-                    log.exception("engine step failed")
-                    self.last_error = f"{type(e).__name__}: {e}"
-                    self.stalled = True
-                    self._step_t0 = None
+                    self._step_failed(e, "engine step failed")
                     continue
                 self._step_t0 = None
                 METRICS.observe_step(time.perf_counter() - t, eng)
                 for r in done:
                     METRICS.observe_request(r)
+
+    def _step_failed(self, e: BaseException, what: str) -> None:
+        """A step raised: mark the service stalled (/healthz 503), answer every in-flight request with an error
+        (done_reason 'error', so no HTTP caller waits for a reply that will never come), then back off before the
+        next step so a persistent fault does not become a hot loop of tracebacks."""
+        self._step_t0 = None
+        self.failures += 1
+        self.last_error = f"{type(e).__name__}: {e}"
+        self.stalled = True
+        if self.failures == 1 or self.failures % 100 == 0:
+            log.exception("%s (failure #%d)", what, self.failures)
+        else:
+            log.error("%s (failure #%d): %s", what, self.failures, self.last_error)
+        failed = self.engine.fail_all(f"engine step failed: {self.last_error}")
+        for r in failed:
+            METRICS.observe_request(r)
+        self._stop.wait(min(self.fail_backoff_s * (2 ** min(self.failures - 1, 6)), 10.0))
 
     def _watch(self) -> None:
         while not self._stop.wait(min(1.0, self.step_deadline_s / 4)):
@@ -214,11 +230,10 @@ class LockstepService(EngineService):
             try:
                 done, _ = self.tpe.step()
             except Exception as e:
-                log.exception("lockstep step failed")
-                self.last_error = f"{type(e).__name__}: {e}"
-                self.stalled = True
-                self._step_t0 = None
-                time.sleep(self.idle_s)
+                # The followers' state is unknown after a failed lockstep step; the leader answers its requests
+                # with errors (the group needs a restart — healthz stays 503).
+                self._step_failed(e, "lockstep step failed")
+                self.tpe.drop_callbacks()
                 continue
             self._step_t0 = None
             if busy:

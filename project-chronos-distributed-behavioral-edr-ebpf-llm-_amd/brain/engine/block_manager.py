@@ -3,7 +3,8 @@ prompt template").
 
 Every CHRONOS prompt starts with the same Llama-3 chat header + "Analyze this sequence. Return JSON ONLY.\\n
 Sequence: [" (chronos_sensor.py:109-111): one full 16-token KV block that every chain would otherwise recompute.
-Full blocks of prompt tokens are content-addressed by a chained hash (parent hash, token ids); a new request reuses
+Full blocks of prompt tokens are content-addressed by a chained SHA-256 digest (parent digest, token ids); a new
+request reuses
 the longest cached run of its prompt's full blocks (refcounted, read-only) and prefills only the remainder.  Blocks
 whose refcount drops to zero stay cached and are recycled least-recently-used when the free list runs dry.
 
@@ -12,6 +13,8 @@ that always runs a fixed number of rows never writes into another sequence's KV.
 """
 from __future__ import annotations
 
+import hashlib
+from array import array
 from collections import OrderedDict
 from typing import Sequence
 
@@ -24,8 +27,8 @@ class BlockManager:
         self.prefix_cache = prefix_cache
         self._free = list(range(num_blocks - 1, 0, -1))
         self._ref: dict[int, int] = {}
-        self._by_hash: dict[int, int] = {}       # content hash -> block
-        self._hash_of: dict[int, int] = {}       # block -> content hash
+        self._by_hash: dict[bytes, int] = {}     # content digest -> block
+        self._hash_of: dict[int, bytes] = {}     # block -> content digest
         self._evictable: "OrderedDict[int, None]" = OrderedDict()  # cached blocks with refcount 0 (LRU order)
         self.hits = 0
         self.lookups = 0
@@ -69,11 +72,14 @@ class BlockManager:
                 self._free.append(b)
 
     # ---- prefix cache ----------------------------------------------------------------------------------------------
-    def _hashes(self, tokens: Sequence[int], nblocks: int) -> list[int]:
-        hs, h = [], 0
+    def _hashes(self, tokens: Sequence[int], nblocks: int) -> list[bytes]:
+        """Chained SHA-256 digests (parent digest || block token ids as int32).  Prompt tokens are partly
+        attacker-controlled (argv paths in the telemetry), so the key must be collision-resistant: a 64-bit
+        non-cryptographic hash collision would hand one prompt another prompt's KV block."""
+        hs, h = [], b""
         bs = self.block_size
         for i in range(nblocks):
-            h = hash((h, tuple(tokens[i * bs:(i + 1) * bs])))
+            h = hashlib.sha256(h + array("i", tokens[i * bs:(i + 1) * bs]).tobytes()).digest()
             hs.append(h)
         return hs
 

@@ -367,6 +367,42 @@ class Engine:
             self.s_ctx[idx] = 1
         return out
 
+    def fail_all(self, error: str) -> list[Request]:
+        """After a step raised: finish every queued, prefilling and decoding request with ``done_reason == 'error'``
+        (callbacks fire, so HTTP callers get an error reply instead of hanging) and return the engine to empty.
+
+        A faulted step may have left the block manager and the prefix cache half-updated, so both are rebuilt rather
+        than patched; the device slot state is reset best-effort (the device itself may be gone)."""
+        with self._lock:
+            reqs = [*self.waiting, *self.prefilling, *self.running.values()]
+            self.waiting.clear()
+            self._cancels = []
+        self.prefilling = []
+        self.running = {}
+        self._pending = None
+        S = self.cfg.max_slots
+        self.free_slots = list(range(S - 1, -1, -1))
+        self.blocks = BlockManager(self.blocks.num_blocks, self.blocks.block_size,
+                                   prefix_cache=self.blocks.prefix_cache)
+        try:
+            self.s_state.fill_(-1)
+            self.s_bt.zero_()
+            self.s_pos.zero_()
+            self.s_ctx.fill_(1)
+        except Exception:  # noqa: BLE001 — a dead device must not stop the error replies below
+            log.exception("slot state reset after a failed step")
+        out = []
+        for r in reqs:
+            if r.done_reason:
+                continue
+            r.slot = -1
+            r.error = error
+            r.meta["internal_error"] = True
+            self.stats["error"] += 1
+            self._finish(r, "error")
+            out.append(r)
+        return out
+
     def run_until_idle(self, max_steps: int = 10**9) -> list[Request]:
         done = []
         for _ in range(max_steps):

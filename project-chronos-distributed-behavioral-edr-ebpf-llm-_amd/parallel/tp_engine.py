@@ -86,6 +86,22 @@ class TPEngine:
         assert self.leader, "cancellations enter through TP rank 0"
         self._cancel_inbox.put((tag, reason))
 
+    def drop_callbacks(self) -> None:
+        """Leader, after a failed step: requests still in the inbox never reached an engine; answer them with an
+        error through their callbacks and forget every live request."""
+        while True:
+            try:
+                s = self._inbox.get_nowait()
+            except queue.Empty:
+                break
+            cb = self._callbacks.pop(s.tag, None)
+            if cb is not None:
+                r = Request(-1, list(s.ids), s.fmt, 0)
+                r.done_reason, r.error = "error", "lockstep step failed"
+                r.meta["internal_error"] = True
+                cb(r)
+        self._reqs.clear()
+
     def _exchange(self, stop: bool = False) -> _Msg:
         msg = _Msg()
         if self.leader:

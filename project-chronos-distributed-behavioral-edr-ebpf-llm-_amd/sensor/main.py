@@ -14,6 +14,7 @@ from __future__ import annotations
 import argparse
 import asyncio
 import sys
+import threading
 import time
 
 from . import render
@@ -58,8 +59,63 @@ def _records_from(source: str) -> bytes:
     raise ValueError(source)
 
 
-def run(argv=None) -> int:
+def _kernel_source(on_records, args):
+    from .loader import KernelSource
+
+    return KernelSource(on_records, page_cnt=args.page_cnt, strict_filter=args.fixed)
+
+
+async def live_async(src_factory, tracker, analyze, render_result, strict: bool = False,
+                     poll_ms: int = 100, stop: "threading.Event | None" = None) -> list[dict]:
+    """Live source with many chains in flight (quirk Q1 fix on the path where the reference actually stalls).
+
+    The perf buffer is polled on one executor thread; records are fed to the tracker on that thread (the tracker is
+    touched by no other thread), and each trigger is handed to the event loop with ``call_soon_threadsafe``, where
+    ``analyze(history)`` runs as its own task.  The poll loop therefore never waits on the Brain, so the per-CPU
+    rings keep draining while requests are in flight.  Ends on KeyboardInterrupt, when ``stop`` is set, or when the
+    source's ``poll`` raises ``EOFError`` (replay-style fake sources); in-flight chains are awaited before return.
+    """
+    loop = asyncio.get_running_loop()
+    tasks: set = set()
+    results: list[dict] = []
+    stop = stop or threading.Event()
+
+    async def one(trig: Trigger):
+        res = await analyze(trig.history)
+        render_result(trig, res)
+        results.append(res)
+
+    def schedule(trig: Trigger):
+        t = loop.create_task(one(trig))
+        tasks.add(t)
+        t.add_done_callback(tasks.discard)
+
+    def on_records(buf: bytes):
+        for trig in tracker.feed_records(buf, kernel_filter=False, strict=strict):
+            loop.call_soon_threadsafe(schedule, trig)
+
+    src = src_factory(on_records)
+
+    def pump():
+        while not stop.is_set():
+            try:
+                src.poll(poll_ms)
+            except (KeyboardInterrupt, EOFError):
+                return
+
+    try:
+        await loop.run_in_executor(None, pump)
+    finally:
+        stop.set()
+    await asyncio.sleep(0)          # let call_soon_threadsafe callbacks queued by the last poll run
+    while tasks:
+        await asyncio.gather(*list(tasks))
+    return results
+
+
+def run(argv=None, src_factory=None) -> int:
     args = _parse(argv)
+    src_factory = src_factory or (lambda on_records: _kernel_source(on_records, args))
     url = _url(args.brain)
     ccfg = ClientConfig(url=url, model=args.model, timeout=args.timeout,
                         fmt=schema_format() if args.schema else "json", retries=2 if args.fixed else 0)
@@ -80,14 +136,12 @@ def run(argv=None) -> int:
                 handle(trig)
 
         if args.source == "bcc":
-            from .loader import KernelSource
-
-            src = KernelSource(lambda b: on_records(b, False), page_cnt=args.page_cnt, strict_filter=strict)
+            src = src_factory(lambda b: on_records(b, False))
             render.emit([render.banner_live()])
             while True:
                 try:
                     src.poll()
-                except KeyboardInterrupt:
+                except (KeyboardInterrupt, EOFError):
                     return 0
         render.emit([render.banner_live()])
         if args.source.startswith("synthetic:"):
@@ -100,6 +154,17 @@ def run(argv=None) -> int:
     # Async: many chains in flight; each chain's block is printed when its verdict arrives.
     async def main_async():
         client = AsyncBrainClient(ccfg, max_inflight=args.inflight)
+        if args.source == "bcc":
+            render.emit([render.banner_live()])
+
+            def show(trig: Trigger, result: dict):
+                render.emit(render.chain_lines(trig.pid, trig.history) + render.verdict_lines(result, args.fixed))
+
+            try:
+                await live_async(src_factory, tracker, client.analyze, show, strict=strict)
+            finally:
+                await client.close()
+            return
         if args.source.startswith("synthetic:"):
             trigs = synthetic_chains(int(args.source.split(":", 1)[1]))
         else:

@@ -252,8 +252,8 @@ def _tp_worker(rank, world, port, q):
     kv2 = KVCache(m.cfg, tp, 16, 16, "cpu")
     out2 = _logits(m, kv2, [list(range(40, 71)), list(range(90, 95)), list(range(7, 30))], [0, 0, 0],
                    [[1, 2], [3], [4, 5]], split=2)
-    if rank == 0:
-        q.put((out, out2))
+    if rank == 0:  # numpy, pickled by value: a torch tensor would be shared through an fd the exiting worker owns
+        q.put((out.numpy(), out2.numpy()))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -275,7 +275,7 @@ def test_tensor_parallel_matches_single():
     ps = [ctx.Process(target=_tp_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in ps:
         p.start()
-    out, out2 = q.get(timeout=240)
+    out, out2 = (torch.from_numpy(a) for a in q.get(timeout=240))
     for p in ps:
         p.join(timeout=60)
     assert torch.allclose(out, ref, atol=3e-2), float((out - ref).abs().max())

@@ -66,7 +66,7 @@ def _worker(rank, world, port, q):
     nblk = (len(req.prompt_ids) + 15) // 16
     blocks = req.blocks[:nblk] if req.blocks else None
     q.put((rank, req.out_ids, req.text, eng.stats["cp_prefill_steps"], len(req.prompt_ids),
-           eng.kv.k[0][:16].clone(), eng.kv.v[1][:16].clone()))
+           eng.kv.k[0][:16].float().numpy(), eng.kv.v[1][:16].float().numpy()))  # by value, not an fd
     dist.barrier()
     dist.destroy_process_group()
 
@@ -96,6 +96,7 @@ def test_cp_engine_matches_single_rank(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     for rank, out_ids, text, cp_steps, plen, k0, v1 in res:
+        k0, v1 = torch.from_numpy(k0), torch.from_numpy(v1)
         assert cp_steps >= 1 and plen == len(r0.prompt_ids)
         json.loads(text)
         assert out_ids == res[0][1]  # lockstep: every rank decodes the same verdict

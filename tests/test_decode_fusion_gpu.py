@@ -309,11 +309,17 @@ def test_input_checks_catch_bad_indices_before_launch():
         ops.set_input_checks(False)
 
 
+@pytest.mark.parametrize("kv", ["bf16", "fp8"])
+@pytest.mark.parametrize("spike", ["big", "small"])
 @pytest.mark.parametrize("variant", [0, 2])
-def test_flash_prefill_forced_rescale(variant):
-    """The flash prefill kernels' rescale paths, forced: late keys whose scores jump far past the running max (v2's
-    deferred-max branch, cdna_hip_programming.md §5.4 rule 26) and a spike against one query row, over a 1200-token
-    chunk on a 900-token prefix; full-tensor fp32 reference."""
+def test_flash_prefill_forced_rescale(variant, spike, kv):
+    """The flash prefill kernels' rescale paths, forced: late keys whose scores jump past the running max, against
+    one query row, over a 1200-token chunk on a 900-token prefix; full-tensor fp32 reference.
+
+    spike="big": the stage max beats the running one by far more than v2's deferred-max threshold (8 in log2 units),
+    so the rescale branch runs.  spike="small": it rises by ~3-4 log2 units, below the threshold, so v2 keeps the
+    stale max and accumulates p up to 2^8 (cdna_hip_programming.md §5.4 rule 26).  kv="fp8" runs the same branches
+    in attn_prefill2_kernel<true> on dequantised e4m3 scores."""
     from chronos import ops
     from chronos.ops import reference as ref
 
@@ -328,15 +334,20 @@ def test_flash_prefill_forced_rescale(variant):
         v = torch.randn(nb, hkv, 128, bs, device=DEV, generator=g).to(torch.bfloat16)
         bt = torch.arange(1, nb, dtype=torch.int32, device=DEV).view(1, -1)
         q = torch.randn(q_lens[0], hq, 128, device=DEV, generator=g).to(torch.bfloat16)
-        # keys 1500..1563 (stage 23) of kv head 3 aligned with q rows: their scores jump ~+40 (log2) past the max
+        # keys 1500..1563 (stage 23) of kv head 3 aligned with q rows: score jump ~+14 (big) / ~+3.5 (small) log2
+        amp = 0.9 if spike == "big" else 0.25
         for t in range(1500, 1564):
-            k[1 + t // bs, 3, t % bs] = (q[t - 900, 12].float() * 0.9).to(torch.bfloat16)
+            k[1 + t // bs, 3, t % bs] = (q[t - 900, 12].float() * amp).to(torch.bfloat16)
+        ks = vs = 1.0
+        if kv == "fp8":
+            ks, vs = 0.25, 0.5
+            k, v = ref.to_fp8_bytes(k, 1 / ks), ref.to_fp8_bytes(v, 1 / vs)
         qs = torch.tensor([0, q_lens[0]], dtype=torch.int32, device=DEV)
         cl = torch.tensor(ctx, dtype=torch.int32, device=DEV)
         tiles = ops.attention_tiles(q_lens, hq, hkv, 8)
         tt = torch.tensor(tiles, dtype=torch.int32, device=DEV).view(-1, 2)
-        out = ops.paged_attention(q, k, v, bt, qs, cl, tt, len(tiles), 8, 1)
-        exp = ref.paged_attention(q, k, v, bt, qs, cl, tt, len(tiles), 8, 1)
+        out = ops.paged_attention(q, k, v, bt, qs, cl, tt, len(tiles), 8, 1, None, ks, vs)
+        exp = ref.paged_attention(q, k, v, bt, qs, cl, tt, len(tiles), 8, 1, None, ks, vs)
         d = (out.float() - exp.float()).abs()
         assert bool((d <= 2e-2 + 2e-2 * exp.float().abs()).all()), float(d.max())
     finally:

@@ -75,6 +75,10 @@ class _SlowEngine:
         self.hang.wait(30)
         raise RuntimeError("device lost")  # the step fails after the hang: health keeps reporting it
 
+    def fail_all(self, error):
+        self.waiting = []
+        return []
+
 
 def test_watchdog_flags_stalled_step_and_healthz_503():
     from chronos.brain.api.service import EngineService
@@ -128,3 +132,56 @@ def test_roctx_ranges_are_noops_without_profiler():
         trace.mark("inside")
     trace.enable(False)
     assert isinstance(avail, bool)
+
+
+class _FaultyEngine:
+    """A real CPU engine whose step raises while requests are queued / prefilling / decoding (a device fault)."""
+
+    def __init__(self, fail_after: int):
+        self.inner = _engine()
+        self.fail_after = fail_after
+        self.steps = 0
+
+    def __getattr__(self, k):
+        return getattr(self.inner, k)
+
+    def step(self):
+        self.steps += 1
+        if self.steps > self.fail_after:
+            raise RuntimeError("HIP error: device lost")
+        return self.inner.step()
+
+
+@pytest.mark.parametrize("fail_after", [0, 1, 3])
+def test_step_exception_fails_inflight_requests_with_error(fail_after):
+    """a raising step must answer every waiting / prefilling / running request with an error
+    (HTTP 500), not leave them hanging while the scheduler hot-loops on the same exception."""
+    from chronos.brain.api.service import EngineService
+
+    eng = _FaultyEngine(fail_after)
+    svc = EngineService(eng, step_deadline_s=60)
+    s = Server(svc)
+    try:
+        import concurrent.futures as cf
+
+        def post(i):
+            return requests.post(f"{s.url}/api/generate", json={"prompt": _prompt(i), "stream": False,
+                                                                 "format": "json",
+                                                                 "options": {"num_predict": 40}}, timeout=60)
+
+        with cf.ThreadPoolExecutor(6) as ex:
+            rs = list(ex.map(post, range(6)))
+        assert all(r.status_code in (200, 500) for r in rs)
+        errs = [r for r in rs if r.status_code == 500]
+        assert errs and all("device lost" in r.json()["error"] for r in errs)
+        assert svc.stalled and svc.failures >= 1
+        assert requests.get(f"{s.url}/healthz", timeout=10).status_code == 503
+        # no hot loop: with nothing in flight the scheduler stops stepping
+        n = eng.steps
+        time.sleep(0.3)
+        assert eng.steps == n
+        # the engine state was reset: all slots free, nothing queued
+        assert not eng.inner.has_work() and len(eng.inner.free_slots) == 4
+    finally:
+        s.close()
+        svc.close()

@@ -40,7 +40,7 @@ def _worker(rank, world, port, q):
     m = build_model("tiny", "cpu", TPContext.from_group(), seed=3)
     la, ka = _logits(m, False)
     ls, ks = _logits(m, True)
-    q.put((rank, la, ls, torch.equal(ka, ks)))
+    q.put((rank, la.numpy(), ls.numpy(), torch.equal(ka, ks)))  # by value (see test_brain_cpu._tp_worker)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -63,6 +63,7 @@ def test_sequence_parallel_matches_allreduce_tp2():
         p.join(timeout=60)
         assert p.exitcode == 0
     for _, la, ls, kv_same in res:
+        la, ls = torch.from_numpy(la), torch.from_numpy(ls)
         assert kv_same  # the local KV-head shard is written identically
         assert torch.allclose(ls, la, atol=1e-2, rtol=1e-2)
         assert (ls - ref).abs().max() <= 0.05 * ref.abs().max() + 0.05
