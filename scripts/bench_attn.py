@@ -40,13 +40,19 @@ def main():
     out = []
     variants = {"legacy": dict(decode_attn_legacy=1, decode_pf=0), "wave": dict(decode_attn_legacy=0, decode_pf=0),
                 "wave_pf": dict(decode_attn_legacy=0, decode_pf=1)}
-    for B, ctx, fp8 in ((1024, 128, False), (1024, 200, False), (256, 160, False), (1024, 512, False),
-                        (64, 1024, False), (1024, 128, True)):
+    ap_shared = int(os.environ.get("ATTN_SHARED_BLOCKS", "0"))
+    cases = ((1024, 128, False), (1024, 200, False), (256, 160, False), (1024, 512, False), (64, 1024, False),
+             (1024, 128, True))
+    if os.environ.get("ATTN_CASES") == "wave":
+        cases = ((1024, 128, False), (1024, 144, False))
+    for B, ctx, fp8 in cases:
         hq, hkv, bs = 32, 8, 16
         nbs = (ctx + bs - 1) // bs
         nb = B * nbs + 1
         perm = torch.randperm(B * nbs, device=dev).to(torch.int32) + 1  # scattered pages, like a live cache
-        bt = perm.view(B, nbs)
+        bt = perm.view(B, nbs).clone()
+        if ap_shared:  # the chat-template prefix: the first blocks are the SAME pages for every sequence
+            bt[:, :ap_shared] = bt[0, :ap_shared]
         if fp8:
             k = torch.randint(0, 120, (nb, hkv, bs, 128), device=dev, dtype=torch.uint8)
             v = torch.randint(0, 120, (nb, hkv, 128, bs), device=dev, dtype=torch.uint8)
@@ -68,7 +74,7 @@ def main():
         ref = outs["legacy"]
         err = max(float((o - ref).abs().max()) for o in outs.values())
         by = int(cl.sum()) * hkv * 128 * 2 * (1 if fp8 else 2)
-        rec = dict(batch=B, ctx=ctx, fp8=fp8, nsplit=ns, **{f"{n}_us": round(t, 1) for n, t in res.items()},
+        rec = dict(batch=B, ctx=ctx, fp8=fp8, nsplit=ns, shared_blocks=ap_shared, **{f"{n}_us": round(t, 1) for n, t in res.items()},
                    **{f"{n}_TBps": round(by / t / 1e6, 2) for n, t in res.items()}, max_diff_vs_legacy=err)
         out.append(rec)
         print(json.dumps(rec), flush=True)
