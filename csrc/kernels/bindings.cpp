@@ -339,7 +339,8 @@ Tensor gemv_resid(const Tensor& x, const Tensor& w, const Tensor& resid_in, cons
 inline chronos::GemvNorm normp_args(const Tensor& s, const Tensor& part, double eps, int64_t M) {
     chk_gpu(part, "part");
     CHK(part.scalar_type() == at::kFloat && part.dim() == 2 && part.size(0) == M, "part must be [M, P] f32");
-    CHK(part.size(1) % 4 == 0 && part.size(1) <= 1024, "part: P % 4 == 0, P <= 1024");
+    CHK(part.size(1) % 4 == 0 && part.size(1) <= (M == 1 ? 2048 : 1024),
+        "part: P % 4 == 0, P <= 2048 (one row) / 1024 (two rows)");
     (void)s;
     chronos::GemvNorm n{};
     n.part = part.data_ptr<float>();

@@ -49,7 +49,8 @@ __device__ __forceinline__ float dot8(const u16x8& w, const u16x8& x, float acc)
 //     inv = rsqrt(sum of the producer's partials / K + eps): the prologue reduces the partials per wave (no barrier,
 //     fixed order) and the epilogue scales the row sums by inv — no norm launch, no per-element work, no extra
 //     bytes over the plain GEMV;
-//   * ROPE epilogue (QKV): workgroup b owns dims {4j..4j+3} and {64+4j..64+4j+3} of head b/16 (j = b%16) — the
+//   * ROPE epilogue (QKV): with P = R/2 rotate-half pairs per workgroup, workgroup b owns dims {Pj..Pj+P-1} and
+//     {64+Pj..64+Pj+P-1} of head b/(64/P) (j = b%(64/P)) — the
 //     rotate-half pairs — so it applies RoPE and writes q to q_out and k, v straight into the paged cache (bf16 or
 //     fp8-e4m3), exactly as rope_kv_write_kernel does from the bf16 qkv output.
 // Together they take a TP=1 decode layer from 9 launches (norm, qkv, rope, attn, combine, o, norm, gate_up, down) to 6.
@@ -62,7 +63,10 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
                                                    const int32_t* __restrict__ gst, int gn) {
     constexpr bool SWIGLU = MODE == kSwiglu;
     constexpr bool ROPE = MODE == kRope || MODE == kRope8;
-    static_assert(!ROPE || R == 8, "rope epilogue: 4 rotate-half pairs per workgroup");
+    static_assert(!ROPE || R == 8 || R == 4 || R == 2, "rope epilogue: R/2 rotate-half pairs per workgroup");
+    constexpr int RP = R / 2;            // rope: rotate-half pairs per workgroup
+    constexpr int RWG = ROPE ? 64 / RP : 1;  // rope: workgroups per head
+    constexpr int NPQ = M == 1 ? 8 : 4;  // NORMP: float4 partials per lane (<= 2048 / 1024 per row)
     constexpr int NR = SWIGLU ? 2 * R : R;  // weight rows streamed by this workgroup
     constexpr int V = NR * M;               // partial sums per lane
     constexpr int DEPTH = (NR + M) * 4 <= 40 ? 3 : 2;  // register ring depth (VGPR budget)
@@ -75,7 +79,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
 #pragma unroll
     for (int r = 0; r < NR; ++r) {
         int row;
-        if constexpr (ROPE) row = (blockIdx.x >> 4) * 128 + (r < 4 ? 0 : 64) + 4 * (blockIdx.x & 15) + (r & 3);
+        if constexpr (ROPE) row = (blockIdx.x / RWG) * 128 + (r < RP ? 0 : 64) + RP * (blockIdx.x % RWG) + (r % RP);
         else row = (SWIGLU && r >= R) ? half + n0 + (r - R) : n0 + r;
         wrow[r] = reinterpret_cast<const u16x8*>(W + (int64_t)row * K);
     }
@@ -95,12 +99,12 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
     };
     // NORMP: the producer's partials (<= 1024 per row) are fetched FIRST, as up to 4 float4 per lane all in flight, so
     // the reduction below waits only for them (vmcnt is in order) and never for the weight ring issued after them
-    float4 pv[M][4];
+    float4 pv[M][NPQ];
     if constexpr (NORMP) {
 #pragma unroll
         for (int m = 0; m < M; ++m)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < NPQ; ++q) {
                 const int i = (q * 64 + lane) * 4;
                 pv[m][q] = (m < mrows && i < nrm.nparts)
                                ? *reinterpret_cast<const float4*>(nrm.part + m * nrm.nparts + i)
@@ -122,7 +126,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
         for (int m = 0; m < M; ++m) {
             float ss = 0.f;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) ss += (pv[m][q].x + pv[m][q].y) + (pv[m][q].z + pv[m][q].w);
+            for (int q = 0; q < NPQ; ++q) ss += (pv[m][q].x + pv[m][q].y) + (pv[m][q].z + pv[m][q].w);
             inv[m] = rsqrtf(wave_sum(ss) / (float)K + nrm.eps);
         }
     }
@@ -154,13 +158,13 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
     };
     auto tot = [&](int i) { return (red[0][i] + red[1][i] + red[2][i] + red[3][i]) * invm(i % M); };
     if constexpr (ROPE) {
-        // thread t < 4*M: pair (r, r+4) of row m; the unfused path rounds the GEMM output to bf16 before RoPE
+        // thread t < RP*M: pair (r, r+RP) of row m; the unfused path rounds the GEMM output to bf16 before RoPE
         const int t = threadIdx.x;
-        if (t >= 4 * M) return;
+        if (t >= RP * M) return;
         const int pr = t / M, m = t % M;
         if (m >= mrows) return;
-        const int unit = blockIdx.x >> 4, d = 4 * (blockIdx.x & 15) + pr;  // head (q | k | v) and dim in [0, 64)
-        const float x1 = bf2f(f2bf(tot(pr * M + m))), x2 = bf2f(f2bf(tot((pr + 4) * M + m)));
+        const int unit = blockIdx.x / RWG, d = RP * (blockIdx.x % RWG) + pr;  // head (q | k | v), dim in [0, 64)
+        const float x1 = bf2f(f2bf(tot(pr * M + m))), x2 = bf2f(f2bf(tot((pr + RP) * M + m)));
         const int p = rp.pos[m];
         const int64_t blk = rp.bt[(int64_t)rp.tok_seq[m] * rp.bt_stride + p / rp.bs];
         const int off = p % rp.bs;
@@ -242,6 +246,25 @@ constexpr int rows_plain() { return M <= 2 ? 8 : 4; }
 template <int M>
 constexpr int rows_swiglu() { return M <= 2 ? 4 : 2; }
 
+// kResid rows per workgroup at M = 1: 8, or 4 / 2 when the knob asks and the consumer's partial reduction (<= 2048
+// per row at M = 1) still covers N / R.  The partials buffer is sized by gemv_resid_parts with the same choice.
+static int resid_rows(int N) {
+    const int r = knob("gemv_r_resid", 8);
+    if (r == 2 && N / 2 <= 2048 && N % 2 == 0) return 2;
+    return (r == 4 && N / 4 <= 2048 && N % 4 == 0) ? 4 : 8;
+}
+
+// Rows per workgroup at M = 1 (one sensor stream), knobs gemv_r_plain / gemv_r_swiglu / gemv_r_resid / gemv_r_rope for
+// in-process A/B; values that are not instantiated fall back to the default.  Isolated kernels on cold weights run
+// 5-13 % faster with fewer rows per workgroup (profiles/r2_gemv_rows.json: LM head 155.6 -> 141 us at R = 2, gate_up
+// 40.7 -> 35.9 us at R = 2), but inside the captured single-stream decode step the defaults below measured best
+// (scripts/single_stream.py --knob-ab: 3.70 ms/token vs 3.74 with (2, 2, 4, 4) and 4.54 with (1, 2, 2, 2);
+// profiles/r2_single_stream_gemv_rows_ab.json), so the measured-best e2e shape stays.
+static int rows_knob(const char* name, int dflt) {
+    const int v = knob(name, dflt);
+    return (v == 1 || v == 2 || v == 4 || v == 8 || v == 16) ? v : dflt;
+}
+
 template <int M>
 static void launch_m(const uint16_t* x, int mrows, int K, const uint16_t* W, int N, uint16_t* y, int mode,
                      const GemvNorm* nrm, const GemvRope* rp, hipStream_t st) {
@@ -256,19 +279,74 @@ static void launch_m(const uint16_t* x, int mrows, int K, const uint16_t* W, int
                        HALF, na, ra, CHRONOS_GATE)
     if (mode == kSwiglu) {
         const int F = N / 2;
+        if constexpr (M == 1) {
+            const int r = rows_knob("gemv_r_swiglu", R2);
+            if (r == 1) {
+                if (np) GV(kSwiglu, true, 1, F, F, F); else GV(kSwiglu, false, 1, F, F, F);
+                return;
+            }
+            if (r == 2 && F % 2 == 0) {
+                if (np) GV(kSwiglu, true, 2, F / 2, F, F); else GV(kSwiglu, false, 2, F / 2, F, F);
+                return;
+            }
+            if (r == 8 && F % 8 == 0) {
+                if (np) GV(kSwiglu, true, 8, F / 8, F, F); else GV(kSwiglu, false, 8, F / 8, F, F);
+                return;
+            }
+        }
         if (np) GV(kSwiglu, true, R2, F / R2, F, F);
         else GV(kSwiglu, false, R2, F / R2, F, F);
     } else if (mode == kPlain) {
+        if constexpr (M == 1) {
+            const int r = rows_knob("gemv_r_plain", R1);
+            if (r == 2 && N % 2 == 0) {
+                if (np) GV(kPlain, true, 2, N / 2, N, 0); else GV(kPlain, false, 2, N / 2, N, 0);
+                return;
+            }
+            if (r == 4 && N % 4 == 0) {
+                if (np) GV(kPlain, true, 4, N / 4, N, 0); else GV(kPlain, false, 4, N / 4, N, 0);
+                return;
+            }
+            if (r == 16 && N % 16 == 0) {
+                if (np) GV(kPlain, true, 16, N / 16, N, 0); else GV(kPlain, false, 16, N / 16, N, 0);
+                return;
+            }
+        }
         if (np) GV(kPlain, true, R1, N / R1, N, 0);
         else GV(kPlain, false, R1, N / R1, N, 0);
     } else if constexpr (M <= 2) {
-        if (mode == kResid) GV(kResid, false, R1, N / R1, N, 0);
-        else if (mode == kRope) {
-            if (np) GV(kRope, true, 8, N / 8, N, 0);
-            else GV(kRope, false, 8, N / 8, N, 0);
+        if (mode == kResid) {
+            const int r = M == 1 ? resid_rows(N) : R1;
+            if constexpr (M == 1) {
+                if (r == 4) {
+                    GV(kResid, false, 4, N / 4, N, 0);
+                    return;
+                }
+                if (r == 2) {
+                    GV(kResid, false, 2, N / 2, N, 0);
+                    return;
+                }
+            }
+            GV(kResid, false, R1, N / R1, N, 0);
         } else {
-            if (np) GV(kRope8, true, 8, N / 8, N, 0);
-            else GV(kRope8, false, 8, N / 8, N, 0);
+            const int r = M == 1 ? rows_knob("gemv_r_rope", 8) : 8;
+            if (mode == kRope) {
+                if (r == 4) {
+                    if (np) GV(kRope, true, 4, N / 4, N, 0); else GV(kRope, false, 4, N / 4, N, 0);
+                } else if (r == 2) {
+                    if (np) GV(kRope, true, 2, N / 2, N, 0); else GV(kRope, false, 2, N / 2, N, 0);
+                } else {
+                    if (np) GV(kRope, true, 8, N / 8, N, 0); else GV(kRope, false, 8, N / 8, N, 0);
+                }
+            } else {
+                if (r == 4) {
+                    if (np) GV(kRope8, true, 4, N / 4, N, 0); else GV(kRope8, false, 4, N / 4, N, 0);
+                } else if (r == 2) {
+                    if (np) GV(kRope8, true, 2, N / 2, N, 0); else GV(kRope8, false, 2, N / 2, N, 0);
+                } else {
+                    if (np) GV(kRope8, true, 8, N / 8, N, 0); else GV(kRope8, false, 8, N / 8, N, 0);
+                }
+            }
         }
     }
 #undef GV
@@ -292,7 +370,7 @@ void launch_gemv_ex(const uint16_t* x, int M, int K, const uint16_t* W, int N, u
     else launch_m<2>(x, M, K, W, N, y, mode, nrm, rope, st);
 }
 
-int gemv_resid_parts(int M, int N) { return N / (M <= 2 ? rows_plain<1>() : rows_plain<4>()); }
+int gemv_resid_parts(int M, int N) { return N / (M == 1 ? resid_rows(N) : M <= 2 ? rows_plain<2>() : rows_plain<4>()); }
 
 int launch_gemv_resid(const uint16_t* x, int M, int K, const uint16_t* W, int N, const uint16_t* rin, uint16_t* rout,
                       float* part_out, hipStream_t st) {

@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--burst", type=int, default=8)
     ap.add_argument("--ab", action="store_true")
     ap.add_argument("--only", choices=list(VARIANTS), default="fused", help="variant without --ab")
+    ap.add_argument("--knob-ab", default=None,
+                    help="';'-separated knob sets ('name=v,name=v'), one fused engine captured under each, interleaved")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
 
@@ -40,11 +42,22 @@ def main():
     from chronos.sensor.prompt import VERDICT_SCHEMA, build_prompt
     from chronos.sensor.replay import synthetic_chains
 
+    from chronos import ops
+
+    ops.load()
     prompts = [build_prompt(c.history) for c in synthetic_chains(a.chains + 1, seed=7)]
     variants = list(VARIANTS) if a.ab else [a.only]
+    knobsets = {}
+    if a.knob_ab:
+        for ks in a.knob_ab.split(";"):
+            kv = dict(x.split("=") for x in ks.split(",") if x)
+            knobsets[ks or "default"] = {k: int(v) for k, v in kv.items()}
+        variants = list(knobsets)
     engines = {}
     for name in variants:
-        fuse, gate = VARIANTS[name]
+        fuse, gate = VARIANTS.get(name, (True, True))
+        for k, v in knobsets.get(name, {}).items():
+            torch.ops.chronos.set_knob(k, v)  # read when this engine's decode graph is captured
         llama._FUSE_NORM = fuse
         eng = Engine(EngineConfig(model=a.model, device="cuda", max_slots=8, max_model_len=512, decode_burst=a.burst,
                                   decode_gate=gate, seed=0))
@@ -52,6 +65,8 @@ def main():
         eng.submit(prompts[0], fmt=VERDICT_SCHEMA, num_predict=a.num_predict)
         eng.run_until_idle()
         engines[name] = (eng, fuse)
+        for k in knobsets.get(name, {}):
+            torch.ops.chronos.set_knob(k, -1)  # back to the built-in default
     res = {name: [] for name in variants}
     for p in prompts[1:]:
         for name, (eng, fuse) in engines.items():
