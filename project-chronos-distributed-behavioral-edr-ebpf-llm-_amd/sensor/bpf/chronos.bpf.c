@@ -6,7 +6,10 @@
  *                                                         comm = the *pre-exec* image name, never filtered
  *   kprobe on the arch openat symbol -> syscall__openat : one OPEN record unless chronos_open_is_noise(path)
  * Records are the 288-byte struct data_t below (ABI mirrored by sensor/abi.py and csrc/sensor_host), pushed to the
- * per-CPU perf array `events`.
+ * per-CPU perf array `events` (the reference's transport, chronos_sensor.py:25,95) or, built with
+ * -DCHRONOS_RINGBUF=<pages>, to ONE BPF ring buffer shared by all CPUs (kernel >= 5.8): records then reach user space
+ * in global submission order instead of drained CPU by CPU (the out-of-order PIDs of the reference screenshot,
+ * SURVEY.md §3.4), with no per-CPU over-provisioning and exact-size samples (no PERF_SAMPLE_RAW padding).
  */
 #include <uapi/linux/ptrace.h>
 #include <linux/sched.h>
@@ -21,7 +24,13 @@ struct data_t {
     char type[CHRONOS_TYPE_LEN];  /* "EXEC" / "OPEN", NUL padded; 2 bytes of tail padding follow */
 };
 
+#ifdef CHRONOS_RINGBUF
+BPF_RINGBUF_OUTPUT(events, CHRONOS_RINGBUF);
+#define CHRONOS_SUBMIT(ctx, d) events.ringbuf_output((d), sizeof(*(d)), 0)
+#else
 BPF_PERF_OUTPUT(events);
+#define CHRONOS_SUBMIT(ctx, d) events.perf_submit((ctx), (d), sizeof(*(d)))
+#endif
 
 static inline __attribute__((always_inline)) void chronos_fill_task(struct data_t *d) {
     d->pid = bpf_get_current_pid_tgid() >> 32;
@@ -37,7 +46,7 @@ int syscall__execve(struct pt_regs *ctx, const char __user *filename,
     if (arg0)
         bpf_probe_read_user_str(&d.argv, sizeof(d.argv), arg0);
     __builtin_memcpy(&d.type, "EXEC", 5);
-    events.perf_submit(ctx, &d, sizeof(d));
+    CHRONOS_SUBMIT(ctx, &d);
     return 0;
 }
 
@@ -48,6 +57,6 @@ int syscall__openat(struct pt_regs *ctx, int dfd, const char __user *filename, i
         return 0;                 /* dropped in kernel: no user-space wake-up */
     chronos_fill_task(&d);
     __builtin_memcpy(&d.type, "OPEN", 5);
-    events.perf_submit(ctx, &d, sizeof(d));
+    CHRONOS_SUBMIT(ctx, &d);
     return 0;
 }

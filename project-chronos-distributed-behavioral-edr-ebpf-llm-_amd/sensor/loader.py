@@ -53,11 +53,28 @@ def make_perf_callback(on_records: Callable[[bytes], None], counters: dict) -> C
     return _cb
 
 
+def ringbuf_cflags(pages: int) -> list[str]:
+    """cflags selecting the BPF ring-buffer transport (one buffer of ``pages`` 4-KiB pages, a power of two)."""
+    if pages <= 0 or pages & (pages - 1):
+        raise ValueError(f"ring buffer pages must be a power of two, got {pages}")
+    return [f"-DCHRONOS_RINGBUF={pages}"]
+
+
 class KernelSource:
-    def __init__(self, on_records: Callable[[bytes], None], page_cnt: int = 64, strict_filter: bool = False):
+    """``transport="perf"``: per-CPU perf rings of ``page_cnt`` pages (the reference).  ``transport="ringbuf"``: one
+    BPF ring buffer of ``page_cnt`` pages shared by all CPUs — global event order across CPUs; a full buffer drops
+    the record in the kernel (``ringbuf_output`` fails), which BCC does not report, so ``lost`` stays 0 there."""
+
+    def __init__(self, on_records: Callable[[bytes], None], page_cnt: int = 64, strict_filter: bool = False,
+                 transport: str = "perf"):
         from bcc import BPF  # noqa: WPS433 — optional dependency, imported lazily
 
         cflags = [f"-I{BPF_DIR}"] + (["-DCHRONOS_FILTER_STRICT"] if strict_filter else [])
+        if transport == "ringbuf":
+            cflags += ringbuf_cflags(page_cnt)
+        elif transport != "perf":
+            raise ValueError(f"transport must be perf or ringbuf, got {transport!r}")
+        self.transport = transport
         self.bpf = BPF(src_file=BPF_SOURCE, cflags=cflags)
         self.bpf.attach_kprobe(event=self.bpf.get_syscall_fnname("execve"), fn_name="syscall__execve")
         self.bpf.attach_kprobe(event=self.bpf.get_syscall_fnname("openat"), fn_name="syscall__openat")
@@ -66,12 +83,18 @@ class KernelSource:
         def _lost(count):
             self.counters["lost"] += count
 
-        self.bpf["events"].open_perf_buffer(make_perf_callback(on_records, self.counters), page_cnt=page_cnt,
-                                            lost_cb=_lost)
+        cb = make_perf_callback(on_records, self.counters)
+        if transport == "ringbuf":
+            self.bpf["events"].open_ring_buffer(lambda ctx, data, size: cb(0, data, size) or 0)
+        else:
+            self.bpf["events"].open_perf_buffer(cb, page_cnt=page_cnt, lost_cb=_lost)
 
     @property
     def lost(self) -> int:
         return self.counters["lost"] + self.counters.get("short", 0)
 
     def poll(self, timeout_ms: int = -1) -> None:
-        self.bpf.perf_buffer_poll(timeout_ms)
+        if self.transport == "ringbuf":
+            self.bpf.ring_buffer_poll(timeout_ms)
+        else:
+            self.bpf.perf_buffer_poll(timeout_ms)

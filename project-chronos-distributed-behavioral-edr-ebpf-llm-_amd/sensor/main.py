@@ -34,7 +34,10 @@ def _parse(argv=None):
     ap.add_argument("--fixed", action="store_true")
     ap.add_argument("--schema", action="store_true", help="send the verdict JSON schema as `format`")
     ap.add_argument("--python-tracker", action="store_true", help="use the pure-Python tracker (oracle)")
-    ap.add_argument("--page-cnt", type=int, default=64)
+    ap.add_argument("--page-cnt", type=int, default=64,
+                    help="perf: pages per CPU ring (reference: 64); ringbuf: pages of the one shared ring")
+    ap.add_argument("--transport", choices=("perf", "ringbuf"), default="perf",
+                    help="kernel -> user channel of the live source (ringbuf: global order across CPUs, kernel >= 5.8)")
     return ap.parse_args(argv)
 
 
@@ -62,7 +65,7 @@ def _records_from(source: str) -> bytes:
 def _kernel_source(on_records, args):
     from .loader import KernelSource
 
-    return KernelSource(on_records, page_cnt=args.page_cnt, strict_filter=args.fixed)
+    return KernelSource(on_records, page_cnt=args.page_cnt, strict_filter=args.fixed, transport=args.transport)
 
 
 async def live_async(src_factory, tracker, analyze, render_result, strict: bool = False,
