@@ -250,6 +250,13 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(
 // on distinct bank quads) and the keys of every 16-key group stored in the P operand's k order
 // [0-3, 8-11, 4-7, 12-15], so each V^T fragment is ONE 16-byte read.  Register-staged K/V for stage s+1 are in
 // flight under stage s, one barrier per stage.
+// LEAN (default): PMC counters showed the kernel VALU-issue-bound, not MFMA- or LDS-bound (SQ_INSTS_VALU ~19.5 per
+// MFMA, profiles/r2_prefill_pmc_v2.txt).  LEAN cuts the per-stage VALU work: the raw v_exp_f32
+// (__builtin_amdgcn_exp2f, no denormal range fix-up), the score scale fused into the exponent's fma and applied to
+// the max instead of to all 32 scores, masking only in edge stages as one compare + select against a per-lane limit
+// (invalid tail rows included), and the staging-register masks only in the stage that reaches past kv_end.
+// 650 -> 876 TFLOP/s on 16k-token chunks over a 48k / 112k prefix, 588 -> 815 causal-only
+// (profiles/r2_prefill_attn_lean.jsonl).
 // ------------------------------------------------------------------------------------------------------------------
 constexpr int kK2Img = 64 * 256;        // K image bytes per stage
 constexpr int kV2Pitch = 144;           // V^T row pitch (bytes)
@@ -257,7 +264,7 @@ constexpr int kV2Img = 128 * kV2Pitch;  // V^T image bytes per stage
 constexpr int kStage2 = kK2Img + kV2Img;
 constexpr float kRescaleThr = 8.f;     // defer-max threshold (log2 units)
 
-template <bool FP8>
+template <bool FP8, bool LEAN>
 __global__ void __launch_bounds__(256, 2) attn_prefill2_kernel(
     const uint16_t* __restrict__ q, const void* __restrict__ kcv, const void* __restrict__ vcv,
     const int32_t* __restrict__ block_table, int bt_stride, const int32_t* __restrict__ q_start,
@@ -327,8 +334,10 @@ __global__ void __launch_bounds__(256, 2) attn_prefill2_kernel(
 #pragma unroll
                 for (int j = 0; j < 4; ++j) ks[j] = p[j];
             }
+            if constexpr (!LEAN) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) ks[j] &= km;
+                for (int j = 0; j < 4; ++j) ks[j] &= km;
+            }
         }
 #pragma unroll
         for (int b = 0; b < 2; ++b) {  // two 16-token pages of this thread's 32-key half
@@ -347,11 +356,28 @@ __global__ void __launch_bounds__(256, 2) attn_prefill2_kernel(
                 vs[2 * b] = p[0];
                 vs[2 * b + 1] = p[1];
             }
-            vs[2 * b] &= vm;
-            vs[2 * b + 1] &= vm;
+            if constexpr (!LEAN) {
+                vs[2 * b] &= vm;
+                vs[2 * b + 1] &= vm;
+            }
         }
     };
-    auto swrite = [&](int buf) {
+    auto swrite = [&](int buf, int s) {
+        if constexpr (LEAN) {
+            // LEAN: the staged keys are masked only in the stage that reaches past kv_end (wave-uniform branch, at
+            // write time when the data is in registers anyway); every other stage writes the loads untouched.
+            if (s * 64 + 64 > kv_end) {
+                const uint16_t km = s * 64 + kkey < kv_end ? 0xFFFF : 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) ks[j] &= km;
+#pragma unroll
+                for (int b = 0; b < 2; ++b) {
+                    const uint16_t vm = s * 64 + vh * 32 + b * 16 < kv_end ? 0xFFFF : 0;
+                    vs[2 * b] &= vm;
+                    vs[2 * b + 1] &= vm;
+                }
+            }
+        }
         unsigned char* base = lds + buf * kStage2;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -377,8 +403,9 @@ __global__ void __launch_bounds__(256, 2) attn_prefill2_kernel(
 
     if (nsteps > 0) {
         gload(0);
-        swrite(0);
+        swrite(0, 0);
     }
+    const bool wave_invalid = __any(rpos < 0);  // tail tile: some rows of this wave are past the chunk end
     __syncthreads();
     for (int s = 0; s < nsteps; ++s) {
         if (s + 1 < nsteps) gload(s + 1);  // in flight under this stage's MFMAs
@@ -401,30 +428,49 @@ __global__ void __launch_bounds__(256, 2) attn_prefill2_kernel(
             sc[kb] = acc;
         }
         // ---- online softmax over this lane's 32 keys + the partner lane's 32 ----
-        const bool edge = (t0 + 64 > kv_end) || (t0 + 63 > wave_min_pos);
+        const bool edge = (t0 + 64 > kv_end) || (t0 + 63 > wave_min_pos) || (LEAN && wave_invalid);
         float mx = -INFINITY;
+        if constexpr (LEAN) {
+            // raw scores (scale > 0 keeps the order): the scale is applied once to the max and fused into the
+            // exponent's fma below.  Masking only in edge stages, as one compare against a per-lane limit
+            // (min(kv_end, rpos + 1); an invalid row has rpos = -1 and masks everything) and a select.
+            if (edge) {
+                const int lim = min(kv_end, rpos + 1) - (t0 + 4 * hf);
 #pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
+                for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                float v = sc[kb][i] * scale_log2;
-                if (edge) {
-                    const int tok = t0 + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * hf;
-                    if (tok >= kv_end || tok > rpos) v = -INFINITY;
-                } else if (rpos < 0) {
-                    v = -INFINITY;
-                }
-                sc[kb][i] = v;
-                mx = fmaxf(mx, v);
+                    for (int i = 0; i < 16; ++i)
+                        sc[kb][i] = (kb * 32 + (i & 3) + 8 * (i >> 2)) >= lim ? -INFINITY : sc[kb][i];
             }
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sc[kb][i]);
+            mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * scale_log2;
+        } else {
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    float v = sc[kb][i] * scale_log2;
+                    if (edge) {
+                        const int tok = t0 + kb * 32 + (i & 3) + 8 * (i >> 2) + 4 * hf;
+                        if (tok >= kv_end || tok > rpos) v = -INFINITY;
+                    } else if (rpos < 0) {
+                        v = -INFINITY;
+                    }
+                    sc[kb][i] = v;
+                    mx = fmaxf(mx, v);
+                }
+            mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        }
         // defer-max (cdna_hip_programming.md T13): O and l are rescaled only when some row's max grew more than
         // kRescaleThr (log2 units) past the max its running sums use — a wave-uniform branch, rare once the causal
         // prefix has been seen; otherwise p = 2^(s - stale max) <= 2^kRescaleThr, exact in f32, fine as bf16.  The
         // decision is taken before this tile's P is formed, so every P.V and l term of the tile sees one factor.
         if (__any(mx > m + kRescaleThr)) {
             const float mnew = fmaxf(m, mx);
-            const float alpha = exp2f(m - mnew);
+            const float alpha = LEAN ? __builtin_amdgcn_exp2f(m - mnew) : exp2f(m - mnew);
             m = mnew;
             lsum *= alpha;
 #pragma unroll
@@ -432,11 +478,13 @@ __global__ void __launch_bounds__(256, 2) attn_prefill2_kernel(
         }
         float ps = 0.f;
         bf16x8 pf[2][2];
+        const float nm = -m;
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                const float p = exp2f(sc[kb][i] - m);
+                // LEAN: the raw v_exp_f32 (no denormal range fix-up: p < 2^-126 flushing to 0 is harmless here)
+                const float p = LEAN ? __builtin_amdgcn_exp2f(fmaf(sc[kb][i], scale_log2, nm)) : exp2f(sc[kb][i] - m);
                 ps += p;
                 pf[kb][i >> 3][i & 7] = (__bf16)p;
             }
@@ -453,7 +501,7 @@ __global__ void __launch_bounds__(256, 2) attn_prefill2_kernel(
                     o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kb][s2], o[db], 0, 0, 0);
                 }
         }
-        if (s + 1 < nsteps) swrite((s + 1) & 1);
+        if (s + 1 < nsteps) swrite((s + 1) & 1, s + 1);
         __syncthreads();
     }
 
@@ -478,24 +526,29 @@ void launch_attn_prefill(const uint16_t* q, const void* kc, const void* vc, cons
                          int ntiles, uint16_t* out, int hq, int hkv, int block_size, float scale, bool fp8,
                          float k_scale, float v_scale, hipStream_t st) {
     if (ntiles == 0) return;
+    // 2 (default): v2 LEAN; 5: v2 as before LEAN (kept for in-process A/B); 0 / 1: the 32-key-step kernel
     const int variant = knob("prefill_variant", 2);
-    if (variant == 2) {
+    if (variant == 2 || variant == 5) {
         static bool attr2 = [] {
-            return hipFuncSetAttribute((const void*)attn_prefill2_kernel<false>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kStage2) == hipSuccess &&
-                   hipFuncSetAttribute((const void*)attn_prefill2_kernel<true>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kStage2) == hipSuccess;
+            bool ok = true;
+            for (const void* f : {(const void*)attn_prefill2_kernel<false, false>,
+                                  (const void*)attn_prefill2_kernel<true, false>,
+                                  (const void*)attn_prefill2_kernel<false, true>,
+                                  (const void*)attn_prefill2_kernel<true, true>})
+                ok &= hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kStage2) == hipSuccess;
+            return ok;
         }();
         (void)attr2;
         const float sl2 = scale * 1.4426950408889634f;
-        if (fp8)
-            hipLaunchKernelGGL(attn_prefill2_kernel<true>, dim3(ntiles, hkv), dim3(256), 2 * kStage2, st, q, kc, vc,
-                               block_table, bt_stride, q_start, ctx_len, tiles, ntiles, out, hq, hkv, block_size, sl2,
-                               k_scale, v_scale);
-        else
-            hipLaunchKernelGGL(attn_prefill2_kernel<false>, dim3(ntiles, hkv), dim3(256), 2 * kStage2, st, q, kc, vc,
-                               block_table, bt_stride, q_start, ctx_len, tiles, ntiles, out, hq, hkv, block_size, sl2,
-                               1.f, 1.f);
+#define AP2_LAUNCH(F, L, KS, VS)                                                                                   \
+    hipLaunchKernelGGL((attn_prefill2_kernel<F, L>), dim3(ntiles, hkv), dim3(256), 2 * kStage2, st, q, kc, vc,     \
+                       block_table, bt_stride, q_start, ctx_len, tiles, ntiles, out, hq, hkv, block_size, sl2, KS, VS)
+        if (variant == 2) {
+            if (fp8) AP2_LAUNCH(true, true, k_scale, v_scale); else AP2_LAUNCH(false, true, 1.f, 1.f);
+        } else {
+            if (fp8) AP2_LAUNCH(true, false, k_scale, v_scale); else AP2_LAUNCH(false, false, 1.f, 1.f);
+        }
+#undef AP2_LAUNCH
         return;
     }
     const int sub = variant == 1 ? 2 : 1;

@@ -68,6 +68,7 @@ def main():
     ap.add_argument("--knob", default="prefill_variant", help="kernel knob the variants are values of")
     ap.add_argument("--out", default=None)
     ap.add_argument("--check", action="store_true", help="compare each variant with the fp32 reference (slow)")
+    ap.add_argument("--cases", default=None, help="comma-separated subset of the case names")
     a = ap.parse_args()
     from chronos import ops
     from chronos.ops import reference as ref
@@ -79,6 +80,8 @@ def main():
         "chunk16k_prefix112k": ([16384], [114688]),
         "wave_176x93": ([93] * 176, [0] * 176),
     }
+    if a.cases:
+        cases = {k: v for k, v in cases.items() if k in a.cases.split(",")}
     variants = [int(x) for x in a.variants.split(",")]
     out = []
     for name, (ql, pf) in cases.items():

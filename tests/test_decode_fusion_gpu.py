@@ -311,7 +311,7 @@ def test_input_checks_catch_bad_indices_before_launch():
 
 @pytest.mark.parametrize("kv", ["bf16", "fp8"])
 @pytest.mark.parametrize("spike", ["big", "small"])
-@pytest.mark.parametrize("variant", [0, 2])
+@pytest.mark.parametrize("variant", [0, 2, 5])
 def test_flash_prefill_forced_rescale(variant, spike, kv):
     """The flash prefill kernels' rescale paths, forced: late keys whose scores jump past the running max, against
     one query row, over a 1200-token chunk on a 900-token prefix; full-tensor fp32 reference.
