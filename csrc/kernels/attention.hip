@@ -326,8 +326,12 @@ __global__ void __launch_bounds__(256) paged_attn_combine_kernel(
 // costs (one 32-token step per wave, then merge); this form is bound by the K/V bytes.  Same MFMA mapping and the
 // same per-step arithmetic order as paged_attn_kernel<1>.
 // ------------------------------------------------------------------------------------------------------------------
-template <bool FP8, bool PF>
-__global__ void __launch_bounds__(256) paged_decode_kernel(
+constexpr float kRescaleThrD = 8.f;  // decode LEAN defer-max threshold (log2 units)
+
+// OCC: minimum workgroups per CU the register allocation must allow (3 = 3 waves per SIMD, <= 168 VGPRs: this
+// kernel is bound by K/V load latency, so more waves in flight is more bytes in flight; 1 = unconstrained)
+template <bool FP8, bool PF, bool LEAN, int OCC>
+__global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
     const uint16_t* __restrict__ q, const void* __restrict__ kcv, const void* __restrict__ vcv,
     const int32_t* __restrict__ block_table, int bt_stride, const int32_t* __restrict__ ctx_len,
     uint16_t* __restrict__ out, int nitems, int hq, int hkv, float scale_log2, float k_scale, float v_scale,
@@ -425,6 +429,50 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
             s[g] = acc;
         }
         float mx = -INFINITY;
+        float alpha = 1.f;
+        float ps = 0.f;
+        bf16x8 pf;
+        if constexpr (LEAN) {
+            // VALU-lean form (as the flash prefill's LEAN): raw scores, masking only in the partial last step, the
+            // scale applied to the max and fused into the exponent's fma, raw v_exp_f32, and the defer-max rescale
+            // (O and l rescaled only when the max grows past kRescaleThrD in log2 units: p <= 2^8 otherwise).
+            if (t0 + 32 > ctx) {
+                const int lim = ctx - (t0 + 4 * h4);
+#pragma unroll
+                for (int g = 0; g < 2; ++g)
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) s[g][i] = (16 * g + i) >= lim ? -INFINITY : s[g][i];
+            }
+#pragma unroll
+            for (int g = 0; g < 2; ++g)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) mx = fmaxf(mx, s[g][i]);
+            mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+            mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * scale_log2;
+            if (__any(mx > m + kRescaleThrD)) {
+                const float mnew = fmaxf(m, mx);
+                alpha = __builtin_amdgcn_exp2f(m - mnew);
+                m = mnew;
+#pragma unroll
+                for (int dt = 0; dt < 8; ++dt) o[dt] *= alpha;
+            }
+            const float nm = -m;
+#pragma unroll
+            for (int g = 0; g < 2; ++g)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    const float p = __builtin_amdgcn_exp2f(fmaf(s[g][i], scale_log2, nm));
+                    ps += p;
+                    pf[4 * g + i] = (__bf16)p;
+                }
+            lsum = lsum * alpha + ps;
+#pragma unroll
+            for (int dt = 0; dt < 8; ++dt) {
+                const bf16x8 va = __builtin_shufflevector(vf[0][dt], vf[1][dt], 0, 1, 2, 3, 4, 5, 6, 7);
+                o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pf, o[dt], 0, 0, 0);
+            }
+            return;
+        }
 #pragma unroll
         for (int g = 0; g < 2; ++g)
 #pragma unroll
@@ -437,10 +485,8 @@ __global__ void __launch_bounds__(256) paged_decode_kernel(
         mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
         mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
         const float mnew = fmaxf(m, mx);
-        const float alpha = exp2f(m - mnew);
+        alpha = exp2f(m - mnew);
         m = mnew;
-        float ps = 0.f;
-        bf16x8 pf;
 #pragma unroll
         for (int g = 0; g < 2; ++g)
 #pragma unroll
@@ -532,14 +578,24 @@ void launch_paged_attn(const uint16_t* q, const void* kc, const void* vc, const 
     if (tiles == nullptr && nqt == 1 && nsplit == 1 && hq / hkv <= 16 && block_size == 16 && nitems >= 2048) {
         if (knob("decode_attn_legacy", 0)) goto legacy;  // A/B against the split-over-waves kernel
         const int pf = knob("decode_pf", 0);
-#define PD_LAUNCH(F, P)                                                                                         \
-    hipLaunchKernelGGL((paged_decode_kernel<F, P>), dim3((nitems + 3) / 4), dim3(256), 0, st, q, kc, vc, block_table, \
-                       bt_stride, ctx_len, out, nitems, hq, hkv, scale_log2, k_scale, v_scale, CHRONOS_GATE)
+        const bool lean = knob("decode_lean", 1) != 0;
+        const bool occ3 = knob("decode_occ3", 1) != 0;
+#define PD_LAUNCH(F, P, L, O)                                                                                   \
+    hipLaunchKernelGGL((paged_decode_kernel<F, P, L, O>), dim3((nitems + 3) / 4), dim3(256), 0, st, q, kc, vc,    \
+                       block_table, bt_stride, ctx_len, out, nitems, hq, hkv, scale_log2, k_scale, v_scale, CHRONOS_GATE)
+#define PD_OCC(F, L)                     \
+    if (occ3) PD_LAUNCH(F, false, L, 3); \
+    else PD_LAUNCH(F, false, L, 1);
         if (fp8) {
-            if (pf) PD_LAUNCH(true, true); else PD_LAUNCH(true, false);
+            if (pf) PD_LAUNCH(true, true, false, 1);
+            else if (lean) { PD_OCC(true, true) }
+            else { PD_OCC(true, false) }
         } else {
-            if (pf) PD_LAUNCH(false, true); else PD_LAUNCH(false, false);
+            if (pf) PD_LAUNCH(false, true, false, 1);
+            else if (lean) { PD_OCC(false, true) }
+            else { PD_OCC(false, false) }
         }
+#undef PD_OCC
 #undef PD_LAUNCH
         return;
     }

@@ -38,7 +38,12 @@ def main():
     C = torch.ops.chronos
     dev = "cuda"
     out = []
-    variants = {"legacy": dict(decode_attn_legacy=1, decode_pf=0), "wave": dict(decode_attn_legacy=0, decode_pf=0),
+    base = dict(decode_attn_legacy=0, decode_pf=0)
+    variants = {"legacy": dict(decode_attn_legacy=1, decode_pf=0),
+                "wave": dict(base, decode_lean=0, decode_occ3=0),
+                "wave_lean": dict(base, decode_lean=1, decode_occ3=0),
+                "wave_occ3": dict(base, decode_lean=0, decode_occ3=1),
+                "wave_lean_occ3": dict(base, decode_lean=1, decode_occ3=1),
                 "wave_pf": dict(decode_attn_legacy=0, decode_pf=1)}
     ap_shared = int(os.environ.get("ATTN_SHARED_BLOCKS", "0"))
     cases = ((1024, 128, False), (1024, 200, False), (256, 160, False), (1024, 512, False), (64, 1024, False),
@@ -80,6 +85,8 @@ def main():
         print(json.dumps(rec), flush=True)
     C.set_knob("decode_attn_legacy", 0)
     C.set_knob("decode_pf", 0)
+    C.set_knob("decode_lean", 1)
+    C.set_knob("decode_occ3", 1)
     if a.out:
         with open(a.out, "w") as fh:
             json.dump(out, fh, indent=1)

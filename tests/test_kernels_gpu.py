@@ -450,3 +450,35 @@ def test_topk_topp_sampling_stays_in_nucleus(tk, tp):
         lgl = torch.where(legal, logits.float().cpu(), -1e30)
         picked = lgl.gather(1, out[:, :1].long().cpu()).squeeze(1)
         assert torch.equal(picked, lgl.max(-1).values)
+
+
+@pytest.mark.parametrize("spike", ["big", "small"])
+def test_decode_one_wave_forced_rescale(spike):
+    """The one-wave decode kernel's defer-max branch (LEAN), forced (cdna_hip_programming.md §5.4 rule 26): in 2048+
+    items, a late key of several sequences is aligned with the query so the score jumps far past the running max
+    (big: the rescale runs) or by less than the 8 (log2) threshold (small: the stale max is kept, p up to 2^8).
+    Every variant (LEAN on / off, occupancy hint on / off) against the full fp32 reference."""
+    from chronos import ops
+    from chronos.ops import reference as ref
+
+    g = torch.Generator().manual_seed(5)
+    ctx_lens = torch.randint(100, 400, (260,), generator=g).tolist()
+    q, k, v, bt, qs, ctx = _attn_case([1] * len(ctx_lens), ctx_lens, 32, 8, 16, seed=31)
+    amp = 4.0 if spike == "big" else 0.1  # score ~ amp * |q|^2 / sqrt(128) * log2(e) ~ amp * 65 (log2)
+    for b in range(0, 260, 7):
+        t = ctx_lens[b] - 3  # in the last 32-key step of the sequence
+        blk = int(bt[b, t // 16])
+        for h in range(8):
+            k[blk, h, t % 16] = (q[b, 4 * h].float() * amp).to(torch.bfloat16)
+    exp = ref.paged_attention(q, k, v, bt, qs, ctx, None, len(ctx_lens), 1, 1)
+    C = torch.ops.chronos
+    try:
+        for lean in (1, 0):
+            for occ in (1, 0):
+                C.set_knob("decode_lean", lean)
+                C.set_knob("decode_occ3", occ)
+                out = ops.paged_attention(q, k, v, bt, qs, ctx, None, len(ctx_lens), 1, 1)
+                _close(out, exp, 2e-2, 2e-2)
+    finally:
+        C.set_knob("decode_lean", 1)
+        C.set_knob("decode_occ3", 1)
