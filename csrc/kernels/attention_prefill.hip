@@ -254,9 +254,12 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(
 // MFMA, profiles/r2_prefill_pmc_v2.txt).  LEAN cuts the per-stage VALU work: the raw v_exp_f32
 // (__builtin_amdgcn_exp2f, no denormal range fix-up), the score scale fused into the exponent's fma and applied to
 // the max instead of to all 32 scores, masking only in edge stages as one compare + select against a per-lane limit
-// (invalid tail rows included), and the staging-register masks only in the stage that reaches past kv_end.
-// 650 -> 876 TFLOP/s on 16k-token chunks over a 48k / 112k prefix, 588 -> 815 causal-only
-// (profiles/r2_prefill_attn_lean.jsonl).
+// (invalid tail rows included), the staging-register masks only in the stage that reaches past kv_end, and staging
+// addresses as one 64-bit block base + a per-thread constant (the general path spent ~100 VALU ops per stage on
+// 64-bit index arithmetic).  650 -> 876 -> 966 TFLOP/s on 16k-token chunks over a 112k prefix, 588 -> 892
+// causal-only (profiles/r2_prefill_attn_lean.jsonl, r2_prefill_attn_lean_staging.jsonl).  Measured and not kept:
+// the stage loop unrolled by LDS buffer (immediate LDS offsets) + block ids fetched a stage ahead: 939-953, within
+// run-to-run noise of the plain loop.
 // ------------------------------------------------------------------------------------------------------------------
 constexpr int kK2Img = 64 * 256;        // K image bytes per stage
 constexpr int kV2Pitch = 144;           // V^T row pitch (bytes)
@@ -313,7 +316,49 @@ __global__ void __launch_bounds__(256, 2) attn_prefill2_kernel(
     // around the loads, so the compiler keeps the staging registers (a branch made it merge them through scratch
     // and wait for the loads right away) and the tile stays in flight under the MFMAs.  Zeroed V keeps stale cache
     // bytes (possibly NaN) out of O even though their P is 0.
+    // LEAN staging addresses (block_size 16, checked by the launcher): a stage's 64 keys are pages s*4 .. s*4+3, so
+    // a thread's page index and in-page offsets are constants plus s*4; the page index is clamped to the last page
+    // (keys past kv_end are zeroed at write time, swrite) and each load address is one 64-bit block base + a
+    // per-thread constant — a handful of VALU ops per stage instead of the general path's 64-bit index arithmetic.
+    const int64_t blk_el = (int64_t)hkv * 16 * kPD;                // elements (bytes for fp8) per cache block
+    const int nblk_m1 = (kv_end + 15) / 16 - 1;
+    const int koffc = (h * 16 + (kkey & 15)) * kPD + kq * 32;      // K: this thread's 64 B of its key
+    const int voffc = (h * kPD + vdim) * 16;                       // V^T: this thread's dim row of a page
+    const int kpg = kkey >> 4, vpg = vh * 2;
+    auto gload_lean = [&](int s) {
+        const int64_t kblk = bt[min(s * 4 + kpg, nblk_m1)];
+        if constexpr (FP8) {
+            const uint4* p = reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(kcv) + kblk * blk_el + koffc);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const uint4 v = p[j];
+                ks[2 * j] = __builtin_bit_cast(u16x8, fp8x8_to_bf16x8(v.x, v.y, k_scale));
+                ks[2 * j + 1] = __builtin_bit_cast(u16x8, fp8x8_to_bf16x8(v.z, v.w, k_scale));
+            }
+        } else {
+            const u16x8* p = reinterpret_cast<const u16x8*>(kc + kblk * blk_el + koffc);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) ks[j] = p[j];
+        }
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const int64_t vblk = bt[min(s * 4 + vpg + b, nblk_m1)];
+            if constexpr (FP8) {
+                const uint4 v = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(vcv) + vblk * blk_el + voffc);
+                vs[2 * b] = __builtin_bit_cast(u16x8, fp8x8_to_bf16x8(v.x, v.y, v_scale));
+                vs[2 * b + 1] = __builtin_bit_cast(u16x8, fp8x8_to_bf16x8(v.z, v.w, v_scale));
+            } else {
+                const u16x8* p = reinterpret_cast<const u16x8*>(vc + vblk * blk_el + voffc);
+                vs[2 * b] = p[0];
+                vs[2 * b + 1] = p[1];
+            }
+        }
+    };
     auto gload = [&](int s) {
+        if constexpr (LEAN) {
+            gload_lean(s);
+            return;
+        }
         const int tok = s * 64 + kkey;
         const bool kval = tok < kv_end;
         const int tk = kval ? tok : 0;
@@ -543,7 +588,7 @@ void launch_attn_prefill(const uint16_t* q, const void* kc, const void* vc, cons
 #define AP2_LAUNCH(F, L, KS, VS)                                                                                   \
     hipLaunchKernelGGL((attn_prefill2_kernel<F, L>), dim3(ntiles, hkv), dim3(256), 2 * kStage2, st, q, kc, vc,     \
                        block_table, bt_stride, q_start, ctx_len, tiles, ntiles, out, hq, hkv, block_size, sl2, KS, VS)
-        if (variant == 2) {
+        if (variant == 2 && block_size == 16) {
             if (fp8) AP2_LAUNCH(true, true, k_scale, v_scale); else AP2_LAUNCH(false, true, 1.f, 1.f);
         } else {
             if (fp8) AP2_LAUNCH(true, false, k_scale, v_scale); else AP2_LAUNCH(false, false, 1.f, 1.f);
