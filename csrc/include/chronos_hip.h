@@ -70,6 +70,16 @@ __device__ __forceinline__ bf16x4 fp8x4_to_bf16x4(uint32_t v, float scale) {
     const f32x2_t hi = __builtin_amdgcn_cvt_pk_f32_fp8((int)v, true);
     return bf16x4{(__bf16)(lo[0] * scale), (__bf16)(lo[1] * scale), (__bf16)(hi[0] * scale), (__bf16)(hi[1] * scale)};
 }
+// Unscaled e4m3 -> bf16 (exact: every e4m3 value is a bf16 value), two per v_cvt_scalef32_pk_bf16_fp8 (gfx950; scale
+// 1.0).  For kernels that fold the cache scale into a later multiply instead of scaling every element.
+__device__ __forceinline__ bf16x8 fp8x8_to_bf16x8_raw(uint32_t v0, uint32_t v1) {
+    typedef __bf16 bf16x2_v __attribute__((ext_vector_type(2)));
+    const bf16x2_v a = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v0, 1.f, false);
+    const bf16x2_v b = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v0, 1.f, true);
+    const bf16x2_v c = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v1, 1.f, false);
+    const bf16x2_v d = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v1, 1.f, true);
+    return bf16x8{a[0], a[1], b[0], b[1], c[0], c[1], d[0], d[1]};
+}
 __device__ __forceinline__ bf16x8 fp8x8_to_bf16x8(uint32_t v0, uint32_t v1, float scale) {
     const bf16x4 a = fp8x4_to_bf16x4(v0, scale), b = fp8x4_to_bf16x4(v1, scale);
     return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);

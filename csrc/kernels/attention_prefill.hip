@@ -272,9 +272,13 @@ __global__ void __launch_bounds__(256, 2) attn_prefill2_kernel(
     const uint16_t* __restrict__ q, const void* __restrict__ kcv, const void* __restrict__ vcv,
     const int32_t* __restrict__ block_table, int bt_stride, const int32_t* __restrict__ q_start,
     const int32_t* __restrict__ ctx_len, const int32_t* __restrict__ tiles, int ntiles, uint16_t* __restrict__ out,
-    int hq, int hkv, int block_size, float scale_log2, float k_scale, float v_scale) {
+    int hq, int hkv, int block_size, float scale_log2_in, float k_scale, float v_scale) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     typedef float f32x16_t __attribute__((ext_vector_type(16)));
+    // LEAN fp8 KV: K/V images hold the unscaled e4m3 values (exact in bf16); k_scale moves into the score scale and
+    // v_scale into the output normalisation, so staging is one conversion per two elements and no multiply.
+    constexpr bool kFold = FP8 && LEAN;
+    const float scale_log2 = kFold ? scale_log2_in * k_scale : scale_log2_in;
     const uint16_t* kc = reinterpret_cast<const uint16_t*>(kcv);
     const uint16_t* vc = reinterpret_cast<const uint16_t*>(vcv);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -332,8 +336,8 @@ __global__ void __launch_bounds__(256, 2) attn_prefill2_kernel(
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 const uint4 v = p[j];
-                ks[2 * j] = __builtin_bit_cast(u16x8, fp8x8_to_bf16x8(v.x, v.y, k_scale));
-                ks[2 * j + 1] = __builtin_bit_cast(u16x8, fp8x8_to_bf16x8(v.z, v.w, k_scale));
+                ks[2 * j] = __builtin_bit_cast(u16x8, fp8x8_to_bf16x8_raw(v.x, v.y));
+                ks[2 * j + 1] = __builtin_bit_cast(u16x8, fp8x8_to_bf16x8_raw(v.z, v.w));
             }
         } else {
             const u16x8* p = reinterpret_cast<const u16x8*>(kc + kblk * blk_el + koffc);
@@ -345,8 +349,8 @@ __global__ void __launch_bounds__(256, 2) attn_prefill2_kernel(
             const int64_t vblk = bt[min(s * 4 + vpg + b, nblk_m1)];
             if constexpr (FP8) {
                 const uint4 v = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(vcv) + vblk * blk_el + voffc);
-                vs[2 * b] = __builtin_bit_cast(u16x8, fp8x8_to_bf16x8(v.x, v.y, v_scale));
-                vs[2 * b + 1] = __builtin_bit_cast(u16x8, fp8x8_to_bf16x8(v.z, v.w, v_scale));
+                vs[2 * b] = __builtin_bit_cast(u16x8, fp8x8_to_bf16x8_raw(v.x, v.y));
+                vs[2 * b + 1] = __builtin_bit_cast(u16x8, fp8x8_to_bf16x8_raw(v.z, v.w));
             } else {
                 const u16x8* p = reinterpret_cast<const u16x8*>(vc + vblk * blk_el + voffc);
                 vs[2 * b] = p[0];
@@ -553,7 +557,7 @@ __global__ void __launch_bounds__(256, 2) attn_prefill2_kernel(
     // ---- epilogue: lane holds O^T[dims 32 db + 8 g + 4 hf + (0..3)][its row] ----
     const float lt = lsum + __shfl_xor(lsum, 32, 64);
     if (!rvalid) return;
-    const float inv = lt > 0.f ? 1.f / lt : 0.f;
+    const float inv = (lt > 0.f ? 1.f / lt : 0.f) * (kFold ? v_scale : 1.f);
     uint16_t* op = out + ((int64_t)(qbase + tr) * hq + hd) * kPD + 4 * hf;
 #pragma unroll
     for (int db = 0; db < 4; ++db)

@@ -69,6 +69,7 @@ def main():
     ap.add_argument("--out", default=None)
     ap.add_argument("--check", action="store_true", help="compare each variant with the fp32 reference (slow)")
     ap.add_argument("--cases", default=None, help="comma-separated subset of the case names")
+    ap.add_argument("--fp8", action="store_true", help="fp8-e4m3 KV cache (k_scale 0.25, v_scale 0.5)")
     a = ap.parse_args()
     from chronos import ops
     from chronos.ops import reference as ref
@@ -86,6 +87,8 @@ def main():
     out = []
     for name, (ql, pf) in cases.items():
         args, flops = case(ql, pf)
+        if a.fp8:
+            args = (args[0], ref.to_fp8_bytes(args[1], 4.0), ref.to_fp8_bytes(args[2], 2.0)) + args[3:] + (None, 0.25, 0.5)
         rec = dict(case=name, tflop=round(flops / 1e12, 2))
         base = None
         for var in variants:

@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--model", default="llama3.1-8b")
     ap.add_argument("--tokens", type=int, default=131000)
     ap.add_argument("--kv-dtype", default="bf16", choices=["bf16", "fp8"])
+    ap.add_argument("--weights", default="bf16", choices=["bf16", "fp8"],
+                    help="fp8: W8A8 e4m3 projections on the block-scaled MFMA (the config's 'CDNA4 fp8 MFMA')")
     ap.add_argument("--chunk", type=int, default=16384)
     ap.add_argument("--num-predict", type=int, default=64)
     ap.add_argument("--device", default="cuda")
@@ -54,7 +56,7 @@ def main():
 
     eng = Engine(EngineConfig(model=a.model, device=a.device, max_slots=1, max_model_len=131072,
                               max_prefill_tokens=a.chunk, kv_dtype=a.kv_dtype, decode_burst=8, prefix_cache=False,
-                              cp_min_tokens=min(4096, a.chunk)),
+                              cp_min_tokens=min(4096, a.chunk), weight_dtype=a.weights),
                  cp=cp)
     # a very long chain: concatenated fleet histories (one process tree that never triggered a reset)
     hist = []
@@ -95,7 +97,8 @@ def main():
         if cp is not None and cp.rank != 0:
             continue
         print(json.dumps({
-            "config": "128k-token kill-chain context", "model": a.model, "kv_dtype": a.kv_dtype, "cp": a.cp,
+            "config": "128k-token kill-chain context", "model": a.model, "kv_dtype": a.kv_dtype,
+            "weights": a.weights, "cp": a.cp,
             "run": rep, "prompt_tokens": len(ids), "ttft_s": round(ttft, 3),
             "prefill_tokens_per_s": round(len(ids) / ttft, 1), "verdict_tokens": len(req.out_ids),
             "decode_ms_per_token": round(1000 * (total - ttft) / max(1, len(req.out_ids)), 2),
