@@ -60,8 +60,8 @@ __device__ __forceinline__ void combine_tile(const float* __restrict__ part_o, c
     }
 }
 
-template <int NQT, bool FP8>
-__global__ void __launch_bounds__(256) paged_attn_kernel(
+template <int NQT, bool FP8, bool PF = false>
+__global__ void __launch_bounds__(256, PF ? 2 : 1) paged_attn_kernel(
     const uint16_t* __restrict__ q, const void* __restrict__ kcv, const void* __restrict__ vcv,
     const int32_t* __restrict__ block_table, int bt_stride, const int32_t* __restrict__ q_start,
     const int32_t* __restrict__ ctx_len, const int32_t* __restrict__ tiles, uint16_t* __restrict__ out,
@@ -135,9 +135,7 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
     }
     const int32_t* bt = block_table + (int64_t)seq * bt_stride;
 
-    for (int t0 = ks + w * 32; t0 < ke; t0 += 128) {
-        bf16x8 kf[2][4];
-        bf16x4 vf[2][8];
+    auto load = [&](int t0, bf16x8 (&kf)[2][4], bf16x4 (&vf)[2][8]) {
 #pragma unroll
         for (int g = 0; g < 2; ++g) {
             const int tg = t0 + 16 * g;
@@ -170,6 +168,8 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
                 for (int dt = 0; dt < 8; ++dt) vf[g][dt] = bf16x4{0, 0, 0, 0};
             }
         }
+    };
+    auto compute = [&](int t0, bf16x8 (&kf)[2][4], bf16x4 (&vf)[2][8]) {
         if (t0 + 32 > ke) {  // partial step: zero V of keys past the end (uniform branch)
 #pragma unroll
             for (int g = 0; g < 2; ++g)
@@ -222,6 +222,26 @@ __global__ void __launch_bounds__(256) paged_attn_kernel(
                 const bf16x8 va = __builtin_shufflevector(vf[0][dt], vf[1][dt], 0, 1, 2, 3, 4, 5, 6, 7);
                 o[qt][dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pf, o[qt][dt], 0, 0, 0);
             }
+        }
+    };
+    if constexpr (PF) {  // decode over long contexts: the wave's next 32-token step (t0 + 128) in flight under this one
+        bf16x8 kA[2][4], kB[2][4];
+        bf16x4 vA[2][8], vB[2][8];
+        int t0 = ks + w * 32;
+        if (t0 < ke) load(t0, kA, vA);
+        for (; t0 < ke; t0 += 256) {
+            if (t0 + 128 < ke) load(t0 + 128, kB, vB);
+            compute(t0, kA, vA);
+            if (t0 + 128 >= ke) break;
+            if (t0 + 256 < ke) load(t0 + 256, kA, vA);
+            compute(t0 + 128, kB, vB);
+        }
+    } else {
+        for (int t0 = ks + w * 32; t0 < ke; t0 += 128) {
+            bf16x8 kf[2][4];
+            bf16x4 vf[2][8];
+            load(t0, kf, vf);
+            compute(t0, kf, vf);
         }
     }
 
@@ -603,12 +623,16 @@ legacy:
     const dim3 grid(ntiles, hkv, nsplit), block(256);
     int* cnt = nsplit > 1 ? tickets_for((int64_t)ntiles * hkv) : nullptr;
     const size_t sh = paged_attn_smem(nqt);
-#define PA_LAUNCH(N, F)                                                                                         \
-    hipLaunchKernelGGL((paged_attn_kernel<N, F>), grid, block, sh, st, q, kc, vc, block_table, bt_stride, q_start, \
-                       ctx_len, tiles, out, part_o, part_lse, hq, hkv, block_size, scale_log2, k_scale, v_scale, \
-                       CHRONOS_GATE, cnt)
+#define PA_LAUNCH(N, F, ...)                                                                                    \
+    hipLaunchKernelGGL((paged_attn_kernel<N, F, ##__VA_ARGS__>), grid, block, sh, st, q, kc, vc, block_table,       \
+                       bt_stride, q_start, ctx_len, tiles, out, part_o, part_lse, hq, hkv, block_size, scale_log2,   \
+                       k_scale, v_scale, CHRONOS_GATE, cnt)
     if (nqt == 1) {
-        if (fp8) PA_LAUNCH(1, true); else PA_LAUNCH(1, false);
+        // decode with a kv split (long contexts): register-prefetch the wave's next 32-token step
+        const bool pf1 = tiles == nullptr && nsplit > 1 && knob("split_pf", 1) != 0;
+        if (pf1) {
+            if (fp8) PA_LAUNCH(1, true, true); else PA_LAUNCH(1, false, true);
+        } else if (fp8) PA_LAUNCH(1, true); else PA_LAUNCH(1, false);
     } else {
         static bool attr = [] {  // > 64 KiB dynamic LDS needs the opt-in (gfx950 has 160 KiB per CU)
             const int b = (int)paged_attn_smem(2);

@@ -50,11 +50,16 @@ def main():
              (1024, 128, True))
     if os.environ.get("ATTN_CASES") == "wave":
         cases = ((1024, 128, False), (1024, 144, False))
+    if os.environ.get("ATTN_CASES") == "long":  # split-K decode over long contexts (the 128k config's decode)
+        cases = ((1, 131072, False), (1, 131072, True), (4, 32768, False), (16, 8192, False), (64, 1024, False))
+        variants = {"split": dict(split_pf=0), "split_pf": dict(split_pf=1)}
     for B, ctx, fp8 in cases:
         hq, hkv, bs = 32, 8, 16
         nbs = (ctx + bs - 1) // bs
         nb = B * nbs + 1
         perm = torch.randperm(B * nbs, device=dev).to(torch.int32) + 1  # scattered pages, like a live cache
+        if os.environ.get("ATTN_SEQ_PAGES"):  # pages in allocation order (a fresh engine's long sequence)
+            perm = torch.arange(B * nbs, device=dev, dtype=torch.int32) + 1
         bt = perm.view(B, nbs).clone()
         if ap_shared:  # the chat-template prefix: the first blocks are the SAME pages for every sequence
             bt[:, :ap_shared] = bt[0, :ap_shared]
@@ -67,6 +72,8 @@ def main():
         q = torch.randn(B, hq, 128, device=dev).to(torch.bfloat16)
         qs = torch.arange(B + 1, device=dev, dtype=torch.int32)
         cl = torch.randint(ctx // 2, ctx + 1, (B,), device=dev, dtype=torch.int32)
+        if os.environ.get("ATTN_CASES") == "long":
+            cl.fill_(ctx)
         ns = ops.pick_nsplit(B * hkv, ctx)
         res = {}
         outs = {}
@@ -76,7 +83,7 @@ def main():
             fn = lambda: ops.paged_attention(q, k, v, bt, qs, cl, None, B, 1, ns)  # noqa: E731
             outs[name] = fn().float()
             res[name] = timeit(fn)
-        ref = outs["legacy"]
+        ref = outs[next(iter(outs))]
         err = max(float((o - ref).abs().max()) for o in outs.values())
         by = int(cl.sum()) * hkv * 128 * 2 * (1 if fp8 else 2)
         rec = dict(batch=B, ctx=ctx, fp8=fp8, nsplit=ns, shared_blocks=ap_shared, **{f"{n}_us": round(t, 1) for n, t in res.items()},
@@ -87,6 +94,7 @@ def main():
     C.set_knob("decode_pf", 0)
     C.set_knob("decode_lean", 1)
     C.set_knob("decode_occ3", 1)
+    C.set_knob("split_pf", 1)
     if a.out:
         with open(a.out, "w") as fh:
             json.dump(out, fh, indent=1)
