@@ -621,7 +621,11 @@ void launch_paged_attn(const uint16_t* q, const void* kc, const void* vc, const 
     }
 legacy:
     const dim3 grid(ntiles, hkv, nsplit), block(256);
-    int* cnt = nsplit > 1 ? tickets_for((int64_t)ntiles * hkv) : nullptr;
+    // in-launch combine (last split merges) only for a few splits: with many splits the per-workgroup agent-scope
+    // release + ticket costs more than the separate combine launch it saves (128k single-sequence decode, 64 splits:
+    // 147 vs 132 us per layer; profiles/r2_attn_split_combine.jsonl)
+    int* cnt = nsplit > 1 && nsplit <= knob("inkernel_combine_max_split", 4) ? tickets_for((int64_t)ntiles * hkv)
+                                                                              : nullptr;
     const size_t sh = paged_attn_smem(nqt);
 #define PA_LAUNCH(N, F, ...)                                                                                    \
     hipLaunchKernelGGL((paged_attn_kernel<N, F, ##__VA_ARGS__>), grid, block, sh, st, q, kc, vc, block_table,       \

@@ -52,7 +52,8 @@ def main():
         cases = ((1024, 128, False), (1024, 144, False))
     if os.environ.get("ATTN_CASES") == "long":  # split-K decode over long contexts (the 128k config's decode)
         cases = ((1, 131072, False), (1, 131072, True), (4, 32768, False), (16, 8192, False), (64, 1024, False))
-        variants = {"split": dict(split_pf=0), "split_pf": dict(split_pf=1)}
+        variants = {"split": dict(split_pf=0, attn_inkernel_combine=1), "split_pf": dict(split_pf=1, attn_inkernel_combine=1),
+                    "split_pf_sepcomb": dict(split_pf=1, attn_inkernel_combine=0)}
     for B, ctx, fp8 in cases:
         hq, hkv, bs = 32, 8, 16
         nbs = (ctx + bs - 1) // bs
@@ -95,6 +96,7 @@ def main():
     C.set_knob("decode_lean", 1)
     C.set_knob("decode_occ3", 1)
     C.set_knob("split_pf", 1)
+    C.set_knob("attn_inkernel_combine", 1)
     if a.out:
         with open(a.out, "w") as fh:
             json.dump(out, fh, indent=1)
