@@ -104,7 +104,8 @@ class EngineService:
         kind = item[0]
         if kind == "submit":
             _, params, ids, on_done, on_tokens, handle = item
-            if handle.get("cancelled"):
+            if handle.get("cancelled"):  # the caller gave up before admission: never enters the engine
+                self.engine.stats["cancelled"] += 1
                 return
             handle["req"] = self.engine.submit(
                 ids, fmt=params.format, num_predict=params.num_predict, temperature=params.temperature,

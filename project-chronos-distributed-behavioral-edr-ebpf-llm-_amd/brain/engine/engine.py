@@ -217,7 +217,7 @@ class Engine:
         self.running: dict[int, Request] = {}
         self.free_slots = list(range(S - 1, -1, -1))
         self._rid = itertools.count()
-        self._graphs: dict[int, torch.cuda.CUDAGraph] = {}
+        self._graphs: dict[tuple[int, int], torch.cuda.CUDAGraph] = {}  # (decode rows, kv splits) -> graph
         self._graph_pool = None
         self.stats = collections.Counter()
         # host wall seconds per scheduler phase (harvest includes harvest_gpu_wait: the wait for the burst to finish)
@@ -548,22 +548,35 @@ class Engine:
                                self.s_temp[:n], self.s_seed[:n], self.s_ids[:n], self.s_pos[:n], self.s_ctx[:n],
                                self.s_nout[:n], self.s_out[:n], self.s_topk[:n], self.s_topp[:n])
 
-    def _nsplit(self, n: int) -> int:
-        return ops.pick_nsplit(n * self.model.hkv, self.cfg.max_model_len)
+    def _nsplit(self, n: int, ctx_cap: int | None = None) -> int:
+        return ops.pick_nsplit(n * self.model.hkv, ctx_cap or self.cfg.max_model_len)
+
+    def _ctx_class(self) -> int:
+        """Power-of-two bound (>= 256, <= max_model_len) on every running sequence's context during the next burst:
+        prompt + num_predict, known at admission.  The decode kv split (flash-decoding) is sized for it, so short
+        verdict contexts decode with one split (no combine) instead of the split count max_model_len would ask for
+        (single stream, 512-token engine: 3.71 -> 3.64 ms/token; profiles/r2_single_stream_split_ab.json), and a
+        128k request still gets its 64."""
+        need = max((len(r.prompt_ids) + r.num_predict for r in self.running.values()), default=1)
+        c = 256
+        while c < need:
+            c *= 2
+        return min(c, self.cfg.max_model_len)
 
     def _decode_burst(self) -> _Snapshot:
         n = min(self._decode_rows(), self.cfg.max_slots)
         k = self.cfg.decode_burst
+        ns = self._nsplit(n, self._ctx_class())
         if self.device.type == "cuda" and self.cfg.use_graphs:
-            g = self._graphs.get(n)
+            g = self._graphs.get((n, ns))
             if g is None:
-                g = self._capture(n)
+                g = self._capture(n, ns)
             g.replay()
         else:
             self._gate(n)
             try:
                 for _ in range(k):
-                    self._decode_once(n, self._nsplit(n))
+                    self._decode_once(n, ns)
             finally:
                 self._gate(0)
         self.stats["decode_steps"] += k
@@ -589,11 +602,10 @@ class Engine:
         if self.device.type == "cuda" and self.cfg.decode_gate:
             ops.set_decode_gate(self.s_state, n if 0 < n <= 8 else 0)
 
-    def _capture(self, n: int) -> "torch.cuda.CUDAGraph":
+    def _capture(self, n: int, ns: int) -> "torch.cuda.CUDAGraph":
         if self._graph_pool is None:
             self._graph_pool = torch.cuda.graph_pool_handle()
         g = torch.cuda.CUDAGraph()
-        ns = self._nsplit(n)
         torch.cuda.synchronize()
         self._gate(n)
         try:
@@ -602,7 +614,7 @@ class Engine:
                     self._decode_once(n, ns)
         finally:
             self._gate(0)
-        self._graphs[n] = g
+        self._graphs[(n, ns)] = g
         self.stats["graphs_captured"] += 1
         return g
 

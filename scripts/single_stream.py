@@ -56,8 +56,12 @@ def main():
     engines = {}
     for name in variants:
         fuse, gate = VARIANTS.get(name, (True, True))
+        saved_split = ops._SPLIT_MAX
         for k, v in knobsets.get(name, {}).items():
-            torch.ops.chronos.set_knob(k, v)  # read when this engine's decode graph is captured
+            if k == "py_split_max":  # decode kv-split cap (ops.pick_nsplit), baked into the captured graph
+                ops._SPLIT_MAX = v
+            else:
+                torch.ops.chronos.set_knob(k, v)  # read when this engine's decode graph is captured
         llama._FUSE_NORM = fuse
         eng = Engine(EngineConfig(model=a.model, device="cuda", max_slots=8, max_model_len=512, decode_burst=a.burst,
                                   decode_gate=gate, seed=0))
@@ -66,7 +70,9 @@ def main():
         eng.run_until_idle()
         engines[name] = (eng, fuse)
         for k in knobsets.get(name, {}):
-            torch.ops.chronos.set_knob(k, -1)  # back to the built-in default
+            if k != "py_split_max":
+                torch.ops.chronos.set_knob(k, -1)  # back to the built-in default
+        ops._SPLIT_MAX = saved_split
     res = {name: [] for name in variants}
     for p in prompts[1:]:
         for name, (eng, fuse) in engines.items():
