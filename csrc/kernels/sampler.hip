@@ -38,7 +38,7 @@ __device__ __forceinline__ uint32_t ord_key(float x) {
     return (b & 0x8000u) ? (~b & 0xFFFFu) : (b | 0x8000u);
 }
 
-template <typename LT>
+template <typename LT, bool VEC>
 __global__ void __launch_bounds__(1024) constrained_sample_kernel(
     const LT* __restrict__ logits, int64_t lstride, const int32_t* __restrict__ row_of_slot, int vocab,
     const int16_t* __restrict__ next, const int16_t* __restrict__ dist, int done_state, int32_t* __restrict__ state,
@@ -169,6 +169,35 @@ __global__ void __launch_bounds__(1024) constrained_sample_kernel(
     // ---- greedy / Gumbel-max over the legal (and, if filtered, surviving) tokens ---------------------------------
     float best = -INFINITY;
     int besti = 0x7fffffff;
+    if (VEC && temp == 0.f && thr == 0 && (vocab & 7) == 0) {
+        // Greedy fast path: 8 consecutive tokens per thread per iteration (16-byte loads of the DFA row and of the
+        // logits), and the dependent dist[] gather only for a token that would beat this thread's best so far
+        // (lazy legality; a thread walks ascending token ids, so ">" keeps the smallest id among equal maxima, and
+        // the reduction below breaks cross-thread ties by id; the first legal token is always taken, as in the
+        // general loop, so an all -inf row still advances).
+        for (int v0 = threadIdx.x * 8; v0 < vocab; v0 += blockDim.x * 8) {
+            const int4 nv = *reinterpret_cast<const int4*>(nx + v0);
+            float x[8];
+            if constexpr (sizeof(LT) == 2) {
+                const u16x8 lv = *reinterpret_cast<const u16x8*>(reinterpret_cast<const uint16_t*>(lg) + v0);
+#pragma unroll
+                for (int j = 0; j < 8; ++j) x[j] = bf2f(lv[j]);
+            } else {
+                const float4 a = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(lg) + v0);
+                const float4 b = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(lg) + v0 + 4);
+                x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+            }
+            const int nw32[4] = {nv.x, nv.y, nv.z, nv.w};
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int ns = (int)(int16_t)(nw32[j >> 1] >> (16 * (j & 1)));
+                if (ns >= 0 && (x[j] > best || besti == 0x7fffffff) && dist[ns] <= budget) {
+                    best = x[j];
+                    besti = v0 + j;
+                }
+            }
+        }
+    } else
     for (int v = threadIdx.x; v < vocab; v += blockDim.x) {
         if (!legal(v)) continue;
         float sc = logit_at<LT>(lg, v);
@@ -228,14 +257,17 @@ void launch_constrained_sample(const void* logits, bool logits_f32, int64_t lstr
                                const int32_t* topk, const float* topp, int32_t* ids, int32_t* pos, int32_t* ctx,
                                int32_t* nout, int32_t* out_tokens, int max_out, hipStream_t st) {
     if (nslots == 0) return;
-    if (logits_f32)
-        hipLaunchKernelGGL(constrained_sample_kernel<float>, dim3(nslots), dim3(1024), 0, st,
-                           (const float*)logits, lstride, row_of_slot, vocab, next, dist, done_state, state, remaining,
-                           temperature, seed, topk, topp, ids, pos, ctx, nout, out_tokens, max_out);
-    else
-        hipLaunchKernelGGL(constrained_sample_kernel<uint16_t>, dim3(nslots), dim3(1024), 0, st,
-                           (const uint16_t*)logits, lstride, row_of_slot, vocab, next, dist, done_state, state,
-                           remaining, temperature, seed, topk, topp, ids, pos, ctx, nout, out_tokens, max_out);
+    const bool vec = knob("sampler_vec", 1) != 0;
+#define CS_LAUNCH(LT, V)                                                                                        \
+    hipLaunchKernelGGL((constrained_sample_kernel<LT, V>), dim3(nslots), dim3(1024), 0, st, (const LT*)logits, \
+                       lstride, row_of_slot, vocab, next, dist, done_state, state, remaining, temperature, seed,  \
+                       topk, topp, ids, pos, ctx, nout, out_tokens, max_out)
+    if (logits_f32) {
+        if (vec) CS_LAUNCH(float, true); else CS_LAUNCH(float, false);
+    } else {
+        if (vec) CS_LAUNCH(uint16_t, true); else CS_LAUNCH(uint16_t, false);
+    }
+#undef CS_LAUNCH
 }
 
 }  // namespace chronos

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--num-predict", type=int, default=64)
     ap.add_argument("--burst", type=int, default=8)
     ap.add_argument("--ab", action="store_true")
+    ap.add_argument("--async-harvest", action="store_true", help="harvest burst k while burst k+1 runs")
     ap.add_argument("--only", choices=list(VARIANTS), default="fused", help="variant without --ab")
     ap.add_argument("--knob-ab", default=None,
                     help="';'-separated knob sets ('name=v,name=v'), one fused engine captured under each, interleaved")
@@ -60,17 +61,20 @@ def main():
         for k, v in knobsets.get(name, {}).items():
             if k == "py_split_max":  # decode kv-split cap (ops.pick_nsplit), baked into the captured graph
                 ops._SPLIT_MAX = v
+            elif k == "py_burst":  # decode steps per captured graph (engine decode_burst)
+                pass
             else:
                 torch.ops.chronos.set_knob(k, v)  # read when this engine's decode graph is captured
         llama._FUSE_NORM = fuse
-        eng = Engine(EngineConfig(model=a.model, device="cuda", max_slots=8, max_model_len=512, decode_burst=a.burst,
-                                  decode_gate=gate, seed=0))
+        burst = knobsets.get(name, {}).get("py_burst", a.burst)
+        eng = Engine(EngineConfig(model=a.model, device="cuda", max_slots=8, max_model_len=512, decode_burst=burst,
+                                  decode_gate=gate, seed=0, async_harvest=a.async_harvest))
         # capture the n=1 graph under this variant's setting
         eng.submit(prompts[0], fmt=VERDICT_SCHEMA, num_predict=a.num_predict)
         eng.run_until_idle()
         engines[name] = (eng, fuse)
         for k in knobsets.get(name, {}):
-            if k != "py_split_max":
+            if not k.startswith("py_"):
                 torch.ops.chronos.set_knob(k, -1)  # back to the built-in default
         ops._SPLIT_MAX = saved_split
     res = {name: [] for name in variants}
