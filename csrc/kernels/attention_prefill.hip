@@ -259,7 +259,9 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(
 // 64-bit index arithmetic).  650 -> 876 -> 966 TFLOP/s on 16k-token chunks over a 112k prefix, 588 -> 892
 // causal-only (profiles/r2_prefill_attn_lean.jsonl, r2_prefill_attn_lean_staging.jsonl).  Measured and not kept:
 // the stage loop unrolled by LDS buffer (immediate LDS offsets) + block ids fetched a stage ahead: 939-953, within
-// run-to-run noise of the plain loop.
+// run-to-run noise of the plain loop; "optimistic" P against the running max before the rescale decision (so the
+// first key block's exponentials could issue under the second block's QK^T): 924-934 vs 934-943, not kept
+// (profiles/r2_prefill_attn_optimistic_not_kept.jsonl).
 // ------------------------------------------------------------------------------------------------------------------
 constexpr int kK2Img = 64 * 256;        // K image bytes per stage
 constexpr int kV2Pitch = 144;           // V^T row pitch (bytes)
@@ -517,26 +519,32 @@ __global__ void __launch_bounds__(256, 2) attn_prefill2_kernel(
         // kRescaleThr (log2 units) past the max its running sums use — a wave-uniform branch, rare once the causal
         // prefix has been seen; otherwise p = 2^(s - stale max) <= 2^kRescaleThr, exact in f32, fine as bf16.  The
         // decision is taken before this tile's P is formed, so every P.V and l term of the tile sees one factor.
-        if (__any(mx > m + kRescaleThr)) {
+        float ps = 0.f;
+        bf16x8 pf[2][2];
+        auto form_p = [&]() {
+            ps = 0.f;
+            const float nm = -m;
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    // LEAN: the raw v_exp_f32 (no denormal range fix-up: p < 2^-126 flushing to 0 is harmless)
+                    const float p = LEAN ? __builtin_amdgcn_exp2f(fmaf(sc[kb][i], scale_log2, nm))
+                                         : exp2f(sc[kb][i] - m);
+                    ps += p;
+                    pf[kb][i >> 3][i & 7] = (__bf16)p;
+                }
+        };
+        auto rescale = [&]() {
             const float mnew = fmaxf(m, mx);
             const float alpha = LEAN ? __builtin_amdgcn_exp2f(m - mnew) : exp2f(m - mnew);
             m = mnew;
             lsum *= alpha;
 #pragma unroll
             for (int db = 0; db < 4; ++db) o[db] *= alpha;
-        }
-        float ps = 0.f;
-        bf16x8 pf[2][2];
-        const float nm = -m;
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                // LEAN: the raw v_exp_f32 (no denormal range fix-up: p < 2^-126 flushing to 0 is harmless here)
-                const float p = LEAN ? __builtin_amdgcn_exp2f(fmaf(sc[kb][i], scale_log2, nm)) : exp2f(sc[kb][i] - m);
-                ps += p;
-                pf[kb][i >> 3][i & 7] = (__bf16)p;
-            }
+        };
+        if (__any(mx > m + kRescaleThr)) rescale();
+        form_p();
         lsum += ps;
         // ---- O^T += V^T . P^T (k-step (kb, s2): keys kb*32 + 16 s2 + 8 (j>>2) + 4 hf + (j&3)) ----
 #pragma unroll
@@ -589,9 +597,10 @@ void launch_attn_prefill(const uint16_t* q, const void* kc, const void* vc, cons
         }();
         (void)attr2;
         const float sl2 = scale * 1.4426950408889634f;
-#define AP2_LAUNCH(F, L, KS, VS)                                                                                   \
-    hipLaunchKernelGGL((attn_prefill2_kernel<F, L>), dim3(ntiles, hkv), dim3(256), 2 * kStage2, st, q, kc, vc,     \
-                       block_table, bt_stride, q_start, ctx_len, tiles, ntiles, out, hq, hkv, block_size, sl2, KS, VS)
+#define AP2_LAUNCH(F, L, KS, VS, ...)                                                                              \
+    hipLaunchKernelGGL((attn_prefill2_kernel<F, L, ##__VA_ARGS__>), dim3(ntiles, hkv), dim3(256), 2 * kStage2, st, q, \
+                       kc, vc, block_table, bt_stride, q_start, ctx_len, tiles, ntiles, out, hq, hkv, block_size, sl2, KS, \
+                       VS)
         if (variant == 2 && block_size == 16) {
             if (fp8) AP2_LAUNCH(true, true, k_scale, v_scale); else AP2_LAUNCH(false, true, 1.f, 1.f);
         } else {
