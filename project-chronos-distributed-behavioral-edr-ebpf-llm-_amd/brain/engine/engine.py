@@ -14,7 +14,8 @@ Replaces what Ollama + llama.cpp did for the reference (SURVEY.md §1.2 N4, §3.
   to detokenize finished verdicts and free + compact slots (``async_harvest`` reads burst k while burst k+1 runs:
   less host time on the critical path, but compaction one burst later — measured slower on the 1024-stream wave).
   Prefill steps never sync and prompts are tokenized at admission one chunk ahead, so the host tokenizes and builds
-  chunk i+1 while the GPU computes chunk i.
+  chunk i+1 while the GPU computes chunk i; after an idle period the chunks ramp up from ``prefill_ramp`` tokens so
+  the GPU is not left waiting for the first chunk's tokenization.
 
 The reference's ``analyze_sequence`` blocked the sensor for one chain at a time (quirk Q1); here thousands of chains
 are in flight and each returns as soon as its own verdict closes.
@@ -77,6 +78,9 @@ class EngineConfig:
     tp_sequence_parallel: bool = False  # TP prefill: reduce-scatter / all-gather around the norms instead of all-reduce
     decode_gate: bool = True       # small buckets: kernels of steps after the last live row finished return at once
     cp_min_tokens: int = 4096      # context parallel (Engine(cp=...)): prefill chunks at least this long are split
+    # First prefill step after the engine was idle covers this many tokens, each later one 4x more, up to the chunk:
+    # the GPU starts on a small chunk while the host tokenizes the next (0 = always full chunks).
+    prefill_ramp: int = 2048
     # token automata compiled at start-up (a first request must not pay the ~4 s vocab walk: the reference's cold-start
     # timeout): "verdict" = the CHRONOS verdict schema the sensor sends, "json" = format:"json"
     warm_formats: tuple = ("verdict", "json")
@@ -149,6 +153,7 @@ class Engine:
         if self.cp.world > 1 and self.tp.world > 1:
             raise ValueError("context parallelism runs on full-weight (TP=1) ranks")
         self._chunk = cfg.max_prefill_tokens * self.cp.world
+        self._ramp = self._chunk  # current prefill step size (see EngineConfig.prefill_ramp)
         self.device = torch.device(cfg.device)
         if self.device.type == "cuda" and self.device.index is None:
             self.device = torch.device("cuda", torch.cuda.current_device())
@@ -361,10 +366,10 @@ class Engine:
         if reset:
             self.free_slots.sort(reverse=True)
             idx = h2d(torch.tensor(reset, dtype=torch.int64), self.device)
-            self.s_state[idx] = -1
-            self.s_bt[idx] = 0
-            self.s_pos[idx] = 0
-            self.s_ctx[idx] = 1
+            self.s_state.index_fill_(0, idx, -1)
+            self.s_bt.index_fill_(0, idx, 0)
+            self.s_pos.index_fill_(0, idx, 0)
+            self.s_ctx.index_fill_(0, idx, 1)
         return out
 
     def fail_all(self, error: str) -> list[Request]:
@@ -421,8 +426,13 @@ class Engine:
     # ------------------------------------------------------------------------------------------------------------
     def _admit(self) -> None:
         slots, rows = [], []
-        # admit about one prefill chunk ahead: the rest stays queued (and untokenized) while that chunk computes
-        budget = self._chunk - sum(len(r.prompt_ids) - r.prefilled for r in self.prefilling)
+        if not self.prefilling and not self.running and self.cfg.prefill_ramp > 0:
+            # Idle engine: nothing is queued on the GPU, so the host's tokenization of a whole chunk would be exposed
+            # (~50 ms for 16k tokens of chains).  Start small and grow 4x per step, so admitting the next step's
+            # prompts always overlaps the current step's prefill.
+            self._ramp = min(self.cfg.prefill_ramp, self._chunk)
+        # admit about one prefill step ahead: the rest stays queued (and untokenized) while that step computes
+        budget = self._ramp - sum(len(r.prompt_ids) - r.prefilled for r in self.prefilling)
         with self._lock:
             while self.waiting and self.free_slots and budget > 0:
                 req = self.waiting[0]
@@ -457,7 +467,8 @@ class Engine:
                 torch.tensor(rows, dtype=torch.int32), self.device)
 
     def _prefill_step(self) -> None:
-        budget = self._chunk
+        budget = self._ramp
+        self._ramp = min(4 * self._ramp, self._chunk)
         chunks, starts, bts, reqs = [], [], [], []
         for req in self.prefilling:
             if budget <= 0:
@@ -504,7 +515,7 @@ class Engine:
         self.s_rem[sl] = dv(torch.tensor([r.num_predict for r in done_reqs], dtype=torch.int32))
         self.s_pos[sl] = dv(plen - 1)
         self.s_ctx[sl] = dv(plen)
-        self.s_nout[sl] = 0
+        self.s_nout.index_fill_(0, sl, 0)
         self.s_temp[sl] = dv(torch.tensor([r.temperature for r in done_reqs], dtype=torch.float32))
         self.s_seed[sl] = dv(torch.tensor([r.seed for r in done_reqs], dtype=torch.int32))
         self.s_topk[sl] = dv(torch.tensor([r.top_k for r in done_reqs], dtype=torch.int32))
@@ -669,10 +680,10 @@ class Engine:
             self._finish(r, "stop" if stop else "length", timed=False)
         self.free_slots.sort(reverse=True)  # lowest slot first keeps the decode bucket small
         idx = h2d(torch.tensor(reset, dtype=torch.int64), self.device)
-        self.s_state[idx] = -1
-        self.s_bt[idx] = 0
-        self.s_pos[idx] = 0
-        self.s_ctx[idx] = 1
+        self.s_state.index_fill_(0, idx, -1)
+        self.s_bt.index_fill_(0, idx, 0)
+        self.s_pos.index_fill_(0, idx, 0)
+        self.s_ctx.index_fill_(0, idx, 1)
         self.stats["completed"] += len(done)
         self.stats["generated_tokens"] += sum(len(r.out_ids) for r in done)
         self._compact()
@@ -697,10 +708,10 @@ class Engine:
         for t in (self.s_ids, self.s_pos, self.s_ctx, self.s_state, self.s_rem, self.s_nout, self.s_seed, self.s_temp,
                   self.s_topk, self.s_topp, self.s_out, self.s_bt):
             t[di] = t[si]
-        self.s_state[si] = -1
-        self.s_bt[si] = 0
-        self.s_pos[si] = 0
-        self.s_ctx[si] = 1
+        self.s_state.index_fill_(0, si, -1)
+        self.s_bt.index_fill_(0, si, 0)
+        self.s_pos.index_fill_(0, si, 0)
+        self.s_ctx.index_fill_(0, si, 1)
         moved = {}
         for s, d in zip(movers, dst):
             r = self.running.pop(s)

@@ -187,6 +187,38 @@ def test_engine_verdicts_are_valid_json(engine):
     assert not engine.running and not engine.prefilling
 
 
+def test_engine_prefill_ramp(tok):
+    """After an idle period the prefill steps grow prefill_ramp, 4x, 16x ... up to max_prefill_tokens, and the
+    verdicts are the ones full-size chunks give."""
+    from chronos.brain.engine.engine import Engine, EngineConfig
+    from chronos.sensor.prompt import VERDICT_SCHEMA, build_prompt
+    from chronos.sensor.replay import synthetic_chains
+
+    prompts = [build_prompt(c.history) for c in synthetic_chains(6, seed=5, native=False)]
+    texts = {}
+    for ramp in (0, 16):
+        eng = Engine(EngineConfig(model="tiny", device="cpu", max_slots=8, max_model_len=384, use_graphs=False,
+                                  decode_burst=4, max_prefill_tokens=256, prefix_cache=False, prefill_ramp=ramp),
+                     tokenizer=tok)
+        sizes = []
+        for _ in range(2):  # the ramp restarts once the engine went idle
+            reqs = [eng.submit(p, fmt=VERDICT_SCHEMA, num_predict=16) for p in prompts]
+            while eng.has_work():
+                before, pre = eng.stats["prefill_tokens"], bool(eng.prefilling or eng.waiting)
+                eng.step()
+                if pre:
+                    sizes.append(eng.stats["prefill_tokens"] - before)
+        texts[ramp] = [r.text for r in reqs]
+        total = sum(len(r.prompt_ids) for r in reqs)
+        if ramp:
+            half = sizes[:len(sizes) // 2]
+            assert half[:3] == [16, 64, 256] and sum(half) == total, sizes
+            assert sizes[len(sizes) // 2] == 16
+        else:
+            assert sizes[0] == 256
+    assert texts[0] == texts[16]
+
+
 def test_engine_json_mode_and_budget(engine):
     r = engine.submit("anything", fmt="json", num_predict=12)
     r2 = engine.submit("free text", fmt=None, num_predict=5, temperature=0.9, seed=3)
