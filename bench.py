@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--no-prefix-cache", action="store_true")
     ap.add_argument("--async-harvest", action="store_true")
     ap.add_argument("--prefill-ramp", type=int, default=2048, help="first prefill step after idle (0 = full chunks)")
+    ap.add_argument("--no-jump-forward", action="store_true", help="decode grammar-forced runs token by token")
     ap.add_argument("--mode", choices=["wave", "closed"], default="wave")
     ap.add_argument("--weights", choices=["bf16", "fp8"], default="bf16",
                     help="fp8 = W8A8 e4m3 projections on the block-scaled MFMA / hipBLASLt fp8 (not the headline)")
@@ -132,7 +133,7 @@ def main():
     cfg = EngineConfig(model=a.model, device=str(device), max_slots=a.streams, max_model_len=a.max_model_len,
                        default_num_predict=a.num_predict, decode_burst=a.burst, use_graphs=not a.no_graphs,
                        prefix_cache=not a.no_prefix_cache, async_harvest=a.async_harvest, seed=0,
-                       prefill_ramp=a.prefill_ramp,
+                       prefill_ramp=a.prefill_ramp, jump_forward=not a.no_jump_forward,
                        weight_dtype=a.weights, tp_sequence_parallel=a.sequence_parallel)
     # TP: the ranks of a replica submit the same chains in the same order and step the same deterministic scheduler,
     # so they stay in lockstep by construction (the serving path adds the leader broadcast of parallel/tp_engine.py)

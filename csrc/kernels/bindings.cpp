@@ -32,7 +32,7 @@ void launch_paged_attn(const uint16_t*, const void*, const void*, const int32_t*
                        const int32_t*, const int32_t*, int, int, int, uint16_t*, float*, float*, int, int, int, float,
                        bool, float, float, hipStream_t);
 void launch_constrained_sample(const void*, bool, int64_t, const int32_t*, int, int, const int16_t*, const int16_t*,
-                               int, int32_t*, int32_t*, const float*, const int32_t*, const int32_t*, const float*,
+                               const int8_t*, int, int32_t*, int32_t*, const float*, const int32_t*, const int32_t*, const float*,
                                int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, int, hipStream_t);
 void launch_gemv(const uint16_t*, int, int, const uint16_t*, int, uint16_t*, bool, hipStream_t);
 void attn_init();
@@ -234,7 +234,8 @@ void constrained_sample(const Tensor& logits, const c10::optional<Tensor>& row_o
                         const Tensor& dist, int64_t done_state, const Tensor& state, const Tensor& remaining,
                         const c10::optional<Tensor>& temperature, const c10::optional<Tensor>& seed, const Tensor& ids,
                         const Tensor& pos, const Tensor& ctx, const Tensor& nout, const Tensor& out_tokens,
-                        const c10::optional<Tensor>& topk, const c10::optional<Tensor>& topp) {
+                        const c10::optional<Tensor>& topk, const c10::optional<Tensor>& topp,
+                        const c10::optional<Tensor>& jump) {
     CHK(logits.is_cuda() && logits.dim() == 2 && logits.stride(1) == 1, "logits [rows, V] row-contiguous");
     CHK(logits.scalar_type() == at::kBFloat16 || logits.scalar_type() == at::kFloat, "logits bf16 or f32");
     chk_gpu(next, "next");
@@ -280,9 +281,15 @@ void constrained_sample(const Tensor& logits, const c10::optional<Tensor>& row_o
         CHK(topp->scalar_type() == at::kFloat && topp->numel() >= n, "topp: f32, one entry per slot");
         pp = topp->data_ptr<float>();
     }
+    const int8_t* jp = nullptr;
+    if (jump.has_value()) {
+        chk_gpu(*jump, "jump");
+        CHK(jump->scalar_type() == at::kChar && jump->numel() == next.size(0), "jump must be int8 [S]");
+        jp = jump->data_ptr<int8_t>();
+    }
     c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
     chronos::launch_constrained_sample(logits.data_ptr(), logits.scalar_type() == at::kFloat, logits.stride(0), rp,
-                                       (int)n, (int)vocab, next.data_ptr<int16_t>(), dist.data_ptr<int16_t>(),
+                                       (int)n, (int)vocab, next.data_ptr<int16_t>(), dist.data_ptr<int16_t>(), jp,
                                        (int)done_state, i32m(state), i32m(remaining), tp, sp, kp, pp, i32m(ids),
                                        i32m(pos), i32m(ctx), i32m(nout), i32m(out_tokens), (int)out_tokens.size(1),
                                        cur_stream());
@@ -538,7 +545,8 @@ TORCH_LIBRARY(chronos, m) {
           "float v_scale=1.0) -> Tensor");
     m.def("constrained_sample(Tensor logits, Tensor? row_of_slot, Tensor next, Tensor dist, int done_state, "
           "Tensor(a!) state, Tensor(b!) remaining, Tensor? temperature, Tensor? seed, Tensor(c!) ids, Tensor(d!) pos, "
-          "Tensor(e!) ctx, Tensor(f!) nout, Tensor(g!) out_tokens, Tensor? topk=None, Tensor? topp=None) -> ()");
+          "Tensor(e!) ctx, Tensor(f!) nout, Tensor(g!) out_tokens, Tensor? topk=None, Tensor? topp=None, "
+          "Tensor? jump=None) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(chronos, CUDA, m) {

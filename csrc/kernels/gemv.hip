@@ -85,6 +85,9 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
     }
     const u16x8* xr = reinterpret_cast<const u16x8*>(x);
     const int xstride = K >> 3;
+    // gn < 0: check the decode gate BEFORE the first weight loads (a closed gate then streams no weights; an open one
+    // pays the state read's latency up front).  gn > 0: after them (below).
+    if (gn < 0 && gate_closed(gst, -gn)) return;
 
     float acc[V];
 #pragma unroll
@@ -116,7 +119,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
     for (int d = 0; d < DEPTH; ++d)
         if (w + 4 * d < nchunk) load(w + 4 * d, d);
     // the decode gate is checked with the first loads already in flight (a closed gate only wastes their bandwidth)
-    if (gate_closed(gst, gn)) return;
+    if (gn > 0 && gate_closed(gst, gn)) return;
     float inv[M];
 #pragma unroll
     for (int m = 0; m < M; ++m) inv[m] = 1.f;
@@ -274,9 +277,14 @@ static void launch_m(const uint16_t* x, int mrows, int K, const uint16_t* W, int
     const GemvNorm na = nrm ? *nrm : nz;
     const GemvRope ra = rp ? *rp : rz;
     const bool np = nrm && nrm->part;  // consumer of a kResid producer
+    const int32_t* gst = g_gate_n > 0 && g_gate_n <= kGateMax ? g_gate_state : nullptr;
+    // early gate by default: a gated single-stream step (after the verdict closed or the row parked for a jump)
+    // costs 0.28 ms instead of 2.25 (the late check let every workgroup issue its first ring of weight loads, which
+    // at K = 4096 is the whole row), and the live step is no slower (3.60 vs 3.72 ms/token; profiles/r2_studies.md)
+    const int gn = gst ? (knob("gemv_early_gate", 1) ? -g_gate_n : g_gate_n) : 0;
 #define GV(MODE_, NP_, RR, GRID, NOUT, HALF)                                                                     \
     hipLaunchKernelGGL((gemv_kernel<M, RR, MODE_, NP_>), dim3(GRID), dim3(256), 0, st, x, mrows, K, W, y, NOUT, \
-                       HALF, na, ra, CHRONOS_GATE)
+                       HALF, na, ra, gst, gn)
     if (mode == kSwiglu) {
         const int F = N / 2;
         if constexpr (M == 1) {

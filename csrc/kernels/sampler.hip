@@ -11,7 +11,12 @@
 //
 // It then advances the per-slot decode state in place — ids, positions, context length, DFA state, budget, output
 // ring — so a captured decode graph can be replayed for many steps with no host round trip.  Rows whose state is
-// DONE (or < 0 = empty slot) are left untouched.
+// DONE (or < 0: -1 = empty slot, <= -2 = parked) are left untouched.
+//
+// Jump-forward (optional `jump[S]` flags): when the sampled token leads into a state whose continuation the grammar
+// forces for several tokens (`, "verdict": "`), the row is parked as state -2 - s instead of s.  A parked row is not
+// live for the sampler or the decode gate; the host harvests it, appends the forced tokens in one small prefill-mode
+// forward (brain/engine/engine.py Engine._jump) and resumes decoding after them.
 #include "chronos_hip.h"
 
 namespace chronos {
@@ -41,7 +46,8 @@ __device__ __forceinline__ uint32_t ord_key(float x) {
 template <typename LT, bool VEC>
 __global__ void __launch_bounds__(1024) constrained_sample_kernel(
     const LT* __restrict__ logits, int64_t lstride, const int32_t* __restrict__ row_of_slot, int vocab,
-    const int16_t* __restrict__ next, const int16_t* __restrict__ dist, int done_state, int32_t* __restrict__ state,
+    const int16_t* __restrict__ next, const int16_t* __restrict__ dist, const int8_t* __restrict__ jump,
+    int done_state, int32_t* __restrict__ state,
     int32_t* __restrict__ remaining, const float* __restrict__ temperature, const int32_t* __restrict__ seed,
     const int32_t* __restrict__ topk, const float* __restrict__ topp,
     int32_t* __restrict__ ids, int32_t* __restrict__ pos, int32_t* __restrict__ ctx, int32_t* __restrict__ nout,
@@ -242,7 +248,7 @@ __global__ void __launch_bounds__(1024) constrained_sample_kernel(
         if (n < max_out) out_tokens[(int64_t)slot * max_out + n] = besti;
         nout[slot] = n + 1;
         remaining[slot] = budget;
-        state[slot] = ns;
+        state[slot] = (jump && ns != done_state && jump[ns]) ? -2 - ns : ns;
         if (ns != done_state) {
             ids[slot] = besti;
             pos[slot] += 1;
@@ -252,7 +258,8 @@ __global__ void __launch_bounds__(1024) constrained_sample_kernel(
 }
 
 void launch_constrained_sample(const void* logits, bool logits_f32, int64_t lstride, const int32_t* row_of_slot,
-                               int nslots, int vocab, const int16_t* next, const int16_t* dist, int done_state,
+                               int nslots, int vocab, const int16_t* next, const int16_t* dist, const int8_t* jump,
+                               int done_state,
                                int32_t* state, int32_t* remaining, const float* temperature, const int32_t* seed,
                                const int32_t* topk, const float* topp, int32_t* ids, int32_t* pos, int32_t* ctx,
                                int32_t* nout, int32_t* out_tokens, int max_out, hipStream_t st) {
@@ -260,7 +267,7 @@ void launch_constrained_sample(const void* logits, bool logits_f32, int64_t lstr
     const bool vec = knob("sampler_vec", 1) != 0;
 #define CS_LAUNCH(LT, V)                                                                                        \
     hipLaunchKernelGGL((constrained_sample_kernel<LT, V>), dim3(nslots), dim3(1024), 0, st, (const LT*)logits, \
-                       lstride, row_of_slot, vocab, next, dist, done_state, state, remaining, temperature, seed,  \
+                       lstride, row_of_slot, vocab, next, dist, jump, done_state, state, remaining, temperature, seed,  \
                        topk, topp, ids, pos, ctx, nout, out_tokens, max_out)
     if (logits_f32) {
         if (vec) CS_LAUNCH(float, true); else CS_LAUNCH(float, false);

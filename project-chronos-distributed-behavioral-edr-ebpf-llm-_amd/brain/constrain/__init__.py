@@ -7,6 +7,12 @@ All grammars live in ONE global state space so a decode batch can mix requests w
 * each grammar appends its states; a request starts in its grammar's start state;
 * the device table ``next[cap, V]`` (int16) and ``dist[cap]`` are preallocated at a fixed capacity, so graphs captured
   against them stay valid when a new schema is registered at run time.
+
+Jump-forward: given the tokenizer's ``encode``, every state from which the grammar forces a byte string (the bytes of
+``, "verdict": "`` after a risk score) gets a canonical token run ``jumps[s] = (tokens, end_state)`` and the device
+flag ``jump[s]``; the sampler parks a row entering such a state and the engine appends the run in one forward
+instead of one decode step per token (Engine._jump).  The run's last token is left to the model (it may merge with
+the free text that follows), except when the run ends the verdict: then it is completed through EOS to DONE.
 """
 from __future__ import annotations
 
@@ -36,7 +42,8 @@ class CompiledGrammar:
 
 class GrammarBank:
     def __init__(self, token_bytes: list[bytes], stop_ids: tuple[int, ...], vocab: int, capacity: int = 2048,
-                 device="cpu", max_string: int = 160, json_depth: int = 3, max_ws: int = 1):
+                 device="cpu", max_string: int = 160, json_depth: int = 3, max_ws: int = 1, encode=None,
+                 jump_min: int = 2):
         self.token_bytes = token_bytes
         self.stop_ids = tuple(stop_ids)
         self.vocab = vocab
@@ -46,6 +53,9 @@ class GrammarBank:
         self.next = torch.full((capacity, vocab), -1, dtype=torch.int16, device=self.device)
         self.dist = torch.full((capacity,), 32767, dtype=torch.int16, device=self.device)
         self.dist[DONE] = 0
+        self.encode, self.jump_min = encode, jump_min
+        self.jump = torch.zeros((capacity,), dtype=torch.int8, device=self.device)
+        self.jumps: dict[int, tuple[tuple[int, ...], int]] = {}  # global state -> (forced tokens, state after them)
         self.used = 1
         self._host_dist: list[int] = [0]
         self._by_key: dict[str, CompiledGrammar] = {}
@@ -103,8 +113,51 @@ class GrammarBank:
                     _COMPILED[(self._fp, key)] = hit
             nxt, dist, dfa = hit
             cg = CompiledGrammar(key, self._append(nxt, dist), dfa.num_states, dfa)
+            if self.encode is not None:
+                self._add_jumps(cg.start, dfa, nxt, dist)
             self._by_key[key] = cg
             return cg
+
+    def _add_jumps(self, base: int, dfa: "G.ByteDFA", nxt: np.ndarray, dist: np.ndarray) -> None:
+        S = dfa.num_states  # local DONE = S
+        trans = dfa.trans
+        live = (trans >= 0) & (dist[np.clip(trans, 0, None)] < 32767)  # bytes that can still reach DONE
+        nlive = live.sum(axis=1)
+        eos = [e for e in self.stop_ids if 0 <= e < nxt.shape[1]]
+        glob = lambda s: DONE if s == S else s + base  # noqa: E731
+        flags = []
+        for q in range(S):
+            data, cur = bytearray(), q
+            while not dfa.accept[cur] and nlive[cur] == 1 and len(data) < 96:
+                b = int(np.flatnonzero(live[cur])[0])
+                data.append(b)
+                cur = int(trans[cur, b])
+            finishing = bool(dfa.accept[cur]) and nlive[cur] == 0
+            try:
+                toks = self.encode(data.decode("utf-8")) if data else []
+            except UnicodeDecodeError:
+                continue
+            run, st = [], q
+            for t in toks:
+                ns = int(nxt[st, t]) if 0 <= t < nxt.shape[1] else -1
+                if ns < 0:
+                    break
+                run.append(t)
+                st = ns
+            if finishing and st == cur and len(run) == len(toks) and eos:
+                run.append(eos[0])
+                st = S
+            elif run:
+                run.pop()  # leave the last token to the model: it may merge with what follows
+                st = q
+                for t in run:
+                    st = int(nxt[st, t])
+            if st == S or len(run) >= self.jump_min:
+                if run:
+                    self.jumps[q + base] = (tuple(run), glob(st))
+                    flags.append(q + base)
+        if flags:
+            self.jump[torch.tensor(flags, dtype=torch.int64).to(self.device)] = 1
 
     # ---- host-side helpers (tests, CPU engine) -----------------------------------------------------------------
     def step(self, state: int, tok: int) -> int:

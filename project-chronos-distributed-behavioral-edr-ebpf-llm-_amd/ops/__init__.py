@@ -213,10 +213,13 @@ def paged_attention(q, k_cache, v_cache, block_table, q_start, ctx_len, tiles=No
 
 
 def constrained_sample(logits, row_of_slot, next_tab, dist, done_state: int, state, remaining, temperature, seed,
-                       ids, pos, ctx, nout, out_tokens, topk=None, topp=None) -> None:
+                       ids, pos, ctx, nout, out_tokens, topk=None, topp=None, jump=None) -> None:
+    """``jump``: optional int8 [S] flags — a row whose sampled token leads into a flagged state is parked as state
+    ``-2 - s`` (csrc/kernels/sampler.hip, Engine._jump)."""
     if _checking(logits):
         st = state.cpu().long()
-        _need(bool(((st >= -1) & (st < next_tab.shape[0])).all()), "constrained_sample: grammar state out of range")
+        S = next_tab.shape[0]
+        _need(bool(((st >= -1 - S) & (st < S)).all()), "constrained_sample: grammar state out of range")
         _need(next_tab.shape[1] <= logits.shape[-1], "constrained_sample: grammar table wider than the logits")
         if row_of_slot is not None:
             rs = row_of_slot.cpu().long()
@@ -225,10 +228,10 @@ def constrained_sample(logits, row_of_slot, next_tab, dist, done_state: int, sta
             _need(state.shape[0] <= logits.shape[0], "constrained_sample: more slots than logits rows")
     if logits.is_cuda:
         _k().constrained_sample(logits, row_of_slot, next_tab, dist, done_state, state, remaining, temperature, seed,
-                                ids, pos, ctx, nout, out_tokens, topk, topp)
+                                ids, pos, ctx, nout, out_tokens, topk, topp, jump)
     else:
         ref.constrained_sample(logits, row_of_slot, next_tab, dist, done_state, state, remaining, temperature, seed,
-                               ids, pos, ctx, nout, out_tokens, topk, topp)
+                               ids, pos, ctx, nout, out_tokens, topk, topp, jump)
 
 
 def attention_tiles(q_lens: list[int], hq: int, hkv: int, nqt: int) -> list[tuple[int, int]]:

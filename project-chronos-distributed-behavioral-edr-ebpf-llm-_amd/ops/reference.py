@@ -185,8 +185,9 @@ def topkp_threshold(logits: torch.Tensor, legal: torch.Tensor, top_k: int, top_p
 
 
 def constrained_sample(logits, row_of_slot, next_tab, dist, done_state: int, state, remaining, temperature, seed,
-                       ids, pos, ctx, nout, out_tokens, topk=None, topp=None) -> None:
-    """Greedy / Gumbel-max sampling restricted by the token DFA; advances the slot state in place (host loop)."""
+                       ids, pos, ctx, nout, out_tokens, topk=None, topp=None, jump=None) -> None:
+    """Greedy / Gumbel-max sampling restricted by the token DFA; advances the slot state in place (host loop).
+    A row entering a state flagged in ``jump`` is parked as ``-2 - state``."""
     n = state.numel()
     V = next_tab.shape[1]
     for slot in range(n):
@@ -223,7 +224,7 @@ def constrained_sample(logits, row_of_slot, next_tab, dist, done_state: int, sta
             out_tokens[slot, k] = tok
         nout[slot] = k + 1
         remaining[slot] = budget
-        state[slot] = ns
+        state[slot] = -2 - ns if (jump is not None and ns != done_state and int(jump[ns])) else ns
         if ns != done_state:
             ids[slot] = tok
             pos[slot] += 1

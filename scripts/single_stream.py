@@ -61,14 +61,15 @@ def main():
         for k, v in knobsets.get(name, {}).items():
             if k == "py_split_max":  # decode kv-split cap (ops.pick_nsplit), baked into the captured graph
                 ops._SPLIT_MAX = v
-            elif k == "py_burst":  # decode steps per captured graph (engine decode_burst)
+            elif k in ("py_burst", "py_jump"):  # engine decode_burst / jump_forward
                 pass
             else:
                 torch.ops.chronos.set_knob(k, v)  # read when this engine's decode graph is captured
         llama._FUSE_NORM = fuse
         burst = knobsets.get(name, {}).get("py_burst", a.burst)
         eng = Engine(EngineConfig(model=a.model, device="cuda", max_slots=8, max_model_len=512, decode_burst=burst,
-                                  decode_gate=gate, seed=0, async_harvest=a.async_harvest))
+                                  decode_gate=gate, seed=0, async_harvest=a.async_harvest,
+                                  jump_forward=bool(knobsets.get(name, {}).get("py_jump", 1))))
         # capture the n=1 graph under this variant's setting
         eng.submit(prompts[0], fmt=VERDICT_SCHEMA, num_predict=a.num_predict)
         eng.run_until_idle()
@@ -78,6 +79,9 @@ def main():
                 torch.ops.chronos.set_knob(k, -1)  # back to the built-in default
         ops._SPLIT_MAX = saved_split
     res = {name: [] for name in variants}
+    for eng, _ in engines.values():
+        eng.phase_s.clear()
+        eng.stats.clear()
     for p in prompts[1:]:
         for name, (eng, fuse) in engines.items():
             llama._FUSE_NORM = fuse
@@ -97,7 +101,12 @@ def main():
                          p90_ms=round(1e3 * sorted(lat)[int(0.9 * (len(lat) - 1))], 2),
                          mean_tokens=round(statistics.mean(toks), 1),
                          ttft_p50_ms=round(1e3 * statistics.median(ttft), 2),
-                         ms_per_token=round(1e3 * sum(x[0] - x[2] for x in rows) / max(1, sum(toks)), 3))
+                         ms_per_token=round(1e3 * sum(x[0] - x[2] for x in rows) / max(1, sum(toks)), 3),
+                         jumps_per_chain=round(engines[name][0].stats["jumps"] / len(rows), 2),
+                         jump_tokens_per_chain=round(engines[name][0].stats["jump_tokens"] / len(rows), 2),
+                         jump_host_ms_per_chain=round(1e3 * engines[name][0].phase_s["jump"] / len(rows), 2),
+                         bursts_per_chain=round(sum(v for k, v in engines[name][0].stats.items()
+                                                    if k.startswith("bursts@")) / len(rows), 2))
     print(json.dumps(out))
     if a.out:
         with open(a.out, "w") as f:

@@ -1,0 +1,136 @@
+"""Jump-forward over grammar-forced token runs (brain/constrain GrammarBank.jumps, Engine._jump, sampler.hip parking).
+
+The CPU engine (tiny model, reference ops) decodes verdicts with and without jump-forward.  Checks: the verdict
+grammar has forced runs; jumps happen and every jumped span is exactly the grammar's run; the verdicts stay valid
+JSON; and — the numerics check — every token the model chose is the greedy legal argmax of a from-scratch forward
+over prompt + output (teacher forcing), so the KV and logits the jump path left behind are the ones plain decoding
+would have produced.
+"""
+from __future__ import annotations
+
+import json
+
+import pytest
+import torch
+
+from chronos.brain.constrain import DONE
+from chronos.models.llama import make_prefill_batch
+
+
+@pytest.fixture(scope="module")
+def tok():
+    from chronos.brain.tokenizer import load_tokenizer
+
+    return load_tokenizer(None)
+
+
+def _engine(tok, jf: bool):
+    from chronos.brain.engine.engine import Engine, EngineConfig
+
+    return Engine(EngineConfig(model="tiny", device="cpu", max_slots=4, max_model_len=384, use_graphs=False,
+                               decode_burst=4, max_prefill_tokens=128, jump_forward=jf), tokenizer=tok)
+
+
+def _prompts(n=3):
+    from chronos.sensor.prompt import build_prompt
+    from chronos.sensor.replay import synthetic_chains
+
+    return [build_prompt(c.history) for c in synthetic_chains(n, seed=11, native=False)]
+
+
+def _teacher_forced_ok(eng, req, tol: float = 1e-2) -> None:
+    """Every model-chosen output token is the greedy legal choice of a fresh full-sequence forward."""
+    seq = req.prompt_ids + req.out_ids
+    blocks = eng.blocks.alloc(eng.blocks.blocks_for(len(seq)))
+    try:
+        sb = make_prefill_batch([seq], [0], [blocks], eng.model.cfg, eng.tp, eng.device,
+                                max_blocks=eng.max_blocks_per_seq, nqt=eng.cfg.prefill_nqt)
+        sb.last_idx = torch.arange(len(seq), dtype=torch.int64, device=eng.device)
+        logits = eng.model.forward(sb, eng.kv).float()
+    finally:
+        eng.blocks.release(blocks)
+    jumped = {j for n0, k in req.meta.get("jump_spans", []) for j in range(n0, n0 + k)}
+    bank = eng.bank
+    state = bank.get(req.fmt).start
+    plen = len(req.prompt_ids)
+    for j, t in enumerate(req.out_ids):
+        nx = bank.next[state].long()
+        if j not in jumped:
+            budget = req.num_predict - j - 1
+            legal = (nx >= 0) & (bank.dist[nx.clamp(min=0)].long() <= budget)
+            lg = logits[plen + j - 1]
+            best = float(lg.masked_fill(~legal, float("-inf")).max())
+            assert bool(legal[t]), f"token {j} illegal"
+            assert float(lg[t]) >= best - tol * (abs(best) + 1.0), f"token {j} is not the greedy choice"
+        state = int(nx[t])
+        assert state >= 0
+    assert state != DONE or req.done_reason == "stop"
+
+
+def test_verdict_grammar_has_forced_runs(tok):
+    from chronos.sensor.prompt import VERDICT_SCHEMA
+
+    eng = _engine(tok, True)
+    cg = eng.bank.get(VERDICT_SCHEMA)
+    runs = {s: v for s, v in eng.bank.jumps.items() if cg.start <= s < cg.start + cg.num_states}
+    assert len(runs) >= 4
+    tb = tok.token_bytes_list()
+    texts = {b"".join(tb[t] for t in run if t < len(tb)) for run, _ in runs.values()}
+    assert any(b"score" in t for t in texts) and any(b"reason" in t or b"on" in t for t in texts)
+    for s, (run, end) in runs.items():  # walking the run through the device table lands on its end state
+        st = s
+        for t in run:
+            st = int(eng.bank.next[st, t])
+        assert st == end and bool(eng.bank.jump[s])
+
+
+def test_jump_forward_matches_teacher_forcing(tok):
+    from chronos.sensor.prompt import VERDICT_SCHEMA
+
+    eng = _engine(tok, True)
+    reqs = [eng.submit(p, fmt=VERDICT_SCHEMA, num_predict=40) for p in _prompts()]
+    eng.run_until_idle()
+    assert eng.stats["jumps"] > 0 and eng.stats["jump_tokens"] >= eng.stats["jumps"]
+    for r in reqs:
+        v = json.loads(r.text)
+        assert set(v) == {"risk_score", "verdict", "reason"}
+        assert r.meta.get("jump_spans")
+        for n0, k in r.meta["jump_spans"]:
+            assert n0 + k <= len(r.out_ids) + 1
+        _teacher_forced_ok(eng, r)
+    assert eng.blocks.free == eng.blocks.num_blocks - 1 and not eng.running
+
+
+def test_no_jump_forward_also_teacher_forced(tok):
+    """The checker itself on plain token-by-token decoding."""
+    from chronos.sensor.prompt import VERDICT_SCHEMA
+
+    eng = _engine(tok, False)
+    reqs = [eng.submit(p, fmt=VERDICT_SCHEMA, num_predict=40) for p in _prompts(2)]
+    eng.run_until_idle()
+    assert eng.stats["jumps"] == 0
+    for r in reqs:
+        json.loads(r.text)
+        _teacher_forced_ok(eng, r)
+
+
+@pytest.mark.gpu
+def test_jump_forward_gpu_graphs_teacher_forced():
+    """GPU engine, captured decode bursts, parking in the HIP sampler: the same properties as on the CPU (bf16 decode
+    vs prefill rounding: looser tie tolerance)."""
+    from chronos.brain.engine.engine import Engine, EngineConfig
+    from chronos.sensor.prompt import VERDICT_SCHEMA
+
+    eng = Engine(EngineConfig(model="small", device="cuda", max_slots=4, max_model_len=256, decode_burst=4))
+    reqs = [eng.submit(p, fmt=VERDICT_SCHEMA, num_predict=48) for p in _prompts()]
+    eng.run_until_idle()
+    assert eng.stats["jumps"] > 0
+    for r in reqs:
+        assert set(json.loads(r.text)) == {"risk_score", "verdict", "reason"}
+        _teacher_forced_ok(eng, r, tol=5e-2)
+    off = Engine(EngineConfig(model="small", device="cuda", max_slots=4, max_model_len=256, decode_burst=4,
+                              jump_forward=False))
+    r0 = off.submit(_prompts(1)[0], fmt=VERDICT_SCHEMA, num_predict=48)
+    off.run_until_idle()
+    assert off.stats["jumps"] == 0
+    json.loads(r0.text)
