@@ -249,10 +249,10 @@ constexpr int rows_plain() { return M <= 2 ? 8 : 4; }
 template <int M>
 constexpr int rows_swiglu() { return M <= 2 ? 4 : 2; }
 
-// kResid rows per workgroup at M = 1: 8, or 4 / 2 when the knob asks and the consumer's partial reduction (<= 2048
-// per row at M = 1) still covers N / R.  The partials buffer is sized by gemv_resid_parts with the same choice.
+// kResid rows per workgroup at M = 1: 4 (or 2 / 8 by knob) while the consumer's partial reduction (<= 2048 per row at
+// M = 1) still covers N / R, else 8.  The partials buffer is sized by gemv_resid_parts with the same choice.
 static int resid_rows(int N) {
-    const int r = knob("gemv_r_resid", 8);
+    const int r = knob("gemv_r_resid", 4);
     if (r == 2 && N / 2 <= 2048 && N % 2 == 0) return 2;
     return (r == 4 && N / 4 <= 2048 && N % 4 == 0) ? 4 : 8;
 }
@@ -260,9 +260,10 @@ static int resid_rows(int N) {
 // Rows per workgroup at M = 1 (one sensor stream), knobs gemv_r_plain / gemv_r_swiglu / gemv_r_resid / gemv_r_rope for
 // in-process A/B; values that are not instantiated fall back to the default.  Isolated kernels on cold weights run
 // 5-13 % faster with fewer rows per workgroup (profiles/r2_gemv_rows.json: LM head 155.6 -> 141 us at R = 2, gate_up
-// 40.7 -> 35.9 us at R = 2), but inside the captured single-stream decode step the defaults below measured best
-// (scripts/single_stream.py --knob-ab: 3.70 ms/token vs 3.74 with (2, 2, 4, 4) and 4.54 with (1, 2, 2, 2);
-// profiles/r2_single_stream_gemv_rows_ab.json), so the measured-best e2e shape stays.
+// 40.7 -> 35.9 us at R = 2), but inside the captured single-stream decode step only the two small-N projections gain:
+// QKV+RoPE and the residual producers at R = 4 (768 -> 1536 and 512 -> 1024 workgroups: one round of 2-3 workgroups
+// per CU is latency-bound) give 3.16-3.18 ms/token against 3.24 for R = 8; gate_up stays at 4 (R = 8: 3.72, R = 2:
+// 3.25) and the plain GEMV at 8 (scripts/single_stream.py --knob-ab, profiles/r2_single_stream_gemv_rows_ab2.json).
 static int rows_knob(const char* name, int dflt) {
     const int v = knob(name, dflt);
     return (v == 1 || v == 2 || v == 4 || v == 8 || v == 16) ? v : dflt;
@@ -337,7 +338,7 @@ static void launch_m(const uint16_t* x, int mrows, int K, const uint16_t* W, int
             }
             GV(kResid, false, R1, N / R1, N, 0);
         } else {
-            const int r = M == 1 ? rows_knob("gemv_r_rope", 8) : 8;
+            const int r = M == 1 ? rows_knob("gemv_r_rope", 4) : 8;
             if (mode == kRope) {
                 if (r == 4) {
                     if (np) GV(kRope, true, 4, N / 4, N, 0); else GV(kRope, false, 4, N / 4, N, 0);
