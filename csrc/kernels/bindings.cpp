@@ -473,9 +473,11 @@ Tensor qlinear(const Tensor& xq, const Tensor& xs, const Tensor& wq, const Tenso
     return y;
 }
 
+// value < 0: forget the setting (the next read takes CHRONOS_<NAME> or the built-in default again)
 void set_knob(const std::string& name, int64_t value) {
     std::lock_guard<std::mutex> lk(chronos::g_knob_mu);
-    chronos::g_knobs[name] = (int)value;
+    if (value < 0) chronos::g_knobs.erase(name);
+    else chronos::g_knobs[name] = (int)value;
 }
 
 // ---- K14 IPC one-shot all-reduce (allreduce.hip); the handle is the C++ object's address as an int

@@ -56,42 +56,46 @@ __device__ __forceinline__ float dot8(const u16x8& w, const u16x8& x, float acc)
 // Together they take a TP=1 decode layer from 9 launches (norm, qkv, rope, attn, combine, o, norm, gate_up, down) to 6.
 enum : int { kPlain = 0, kSwiglu = 1, kRope = 2, kRope8 = 3, kResid = 4 };
 
+// gemv_kernel: row group g = R output rows.  One group per workgroup (grid = ngroups), or — knob gemv_persist — a
+// smaller grid whose workgroups loop over groups g, g + grid, ...  In the loop the NEXT group's first weight ring is
+// issued as soon as the current group's last dot products have consumed the ring, so its loads are in flight during
+// the current group's cross-wave reduction, barrier and epilogue (the weight stream does not stop between groups).
 template <int M, int R, int MODE, bool NORMP>
 __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ x, int mrows, int K,
                                                    const uint16_t* __restrict__ W, uint16_t* __restrict__ y,
                                                    int nout, int half, GemvNorm nrm, GemvRope rp,
-                                                   const int32_t* __restrict__ gst, int gn) {
+                                                   const int32_t* __restrict__ gst, int gn, int ngroups) {
     constexpr bool SWIGLU = MODE == kSwiglu;
     constexpr bool ROPE = MODE == kRope || MODE == kRope8;
     static_assert(!ROPE || R == 8 || R == 4 || R == 2, "rope epilogue: R/2 rotate-half pairs per workgroup");
     constexpr int RP = R / 2;            // rope: rotate-half pairs per workgroup
     constexpr int RWG = ROPE ? 64 / RP : 1;  // rope: workgroups per head
     constexpr int NPQ = M == 1 ? 8 : 4;  // NORMP: float4 partials per lane (<= 2048 / 1024 per row)
-    constexpr int NR = SWIGLU ? 2 * R : R;  // weight rows streamed by this workgroup
+    constexpr int NR = SWIGLU ? 2 * R : R;  // weight rows streamed per group
     constexpr int V = NR * M;               // partial sums per lane
     constexpr int DEPTH = (NR + M) * 4 <= 40 ? 3 : 2;  // register ring depth (VGPR budget)
-    __shared__ float red[4][V];
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int n0 = blockIdx.x * R;
-    const int nchunk = K >> 9;  // 512-element (1 KiB) chunks per row
-    // row bases are wave-uniform (SGPR pairs); the per-lane part is one 32-bit offset (lane + 64 * chunk) * 16 B
-    const u16x8* wrow[NR];
-#pragma unroll
-    for (int r = 0; r < NR; ++r) {
-        int row;
-        if constexpr (ROPE) row = (blockIdx.x / RWG) * 128 + (r < RP ? 0 : 64) + RP * (blockIdx.x % RWG) + (r % RP);
-        else row = (SWIGLU && r >= R) ? half + n0 + (r - R) : n0 + r;
-        wrow[r] = reinterpret_cast<const u16x8*>(W + (int64_t)row * K);
-    }
-    const u16x8* xr = reinterpret_cast<const u16x8*>(x);
-    const int xstride = K >> 3;
     // gn < 0: check the decode gate BEFORE the first weight loads (a closed gate then streams no weights; an open one
     // pays the state read's latency up front).  gn > 0: after them (below).
     if (gn < 0 && gate_closed(gst, -gn)) return;
-
-    float acc[V];
+    int g = blockIdx.x;
+    if (g >= ngroups) return;
+    __shared__ float red[4][V];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int nchunk = K >> 9;  // 512-element (1 KiB) chunks per row
+    // row bases are wave-uniform (SGPR pairs); the per-lane part is one 32-bit offset (lane + 64 * chunk) * 16 B
+    const u16x8* wrow[NR];
+    auto set_rows = [&](int bid) {
+        const int n0 = bid * R;
 #pragma unroll
-    for (int i = 0; i < V; ++i) acc[i] = 0.f;
+        for (int r = 0; r < NR; ++r) {
+            int row;
+            if constexpr (ROPE) row = (bid / RWG) * 128 + (r < RP ? 0 : 64) + RP * (bid % RWG) + (r % RP);
+            else row = (SWIGLU && r >= R) ? half + n0 + (r - R) : n0 + r;
+            wrow[r] = reinterpret_cast<const u16x8*>(W + (int64_t)row * K);
+        }
+    };
+    const u16x8* xr = reinterpret_cast<const u16x8*>(x);
+    const int xstride = K >> 3;
     u16x8 wr[DEPTH][NR], xv[DEPTH][M];
     auto load = [&](int c, int d) {
         const int off = c * 64 + lane;
@@ -100,8 +104,15 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
 #pragma unroll
         for (int m = 0; m < M; ++m) xv[d][m] = m < mrows ? xr[m * xstride + off] : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
     };
-    // NORMP: the producer's partials (<= 1024 per row) are fetched FIRST, as up to 4 float4 per lane all in flight, so
-    // the reduction below waits only for them (vmcnt is in order) and never for the weight ring issued after them
+    // wave w takes chunks w, w+4, w+8, ... of every row
+    auto prologue = [&]() {
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d)
+            if (w + 4 * d < nchunk) load(w + 4 * d, d);
+    };
+    // NORMP: the producer's partials (<= 1024 per row; the same for every group) are fetched FIRST, as up to 4
+    // float4 per lane all in flight, so the reduction below waits only for them (vmcnt is in order) and never for
+    // the weight ring issued after them
     float4 pv[M][NPQ];
     if constexpr (NORMP) {
 #pragma unroll
@@ -114,11 +125,9 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
                                : float4{0.f, 0.f, 0.f, 0.f};
             }
     }
-    // wave w takes chunks w, w+4, w+8, ...
-#pragma unroll
-    for (int d = 0; d < DEPTH; ++d)
-        if (w + 4 * d < nchunk) load(w + 4 * d, d);
-    // the decode gate is checked with the first loads already in flight (a closed gate only wastes their bandwidth)
+    set_rows(g);
+    prologue();
+    // late gate: checked with the first loads already in flight (a closed gate then wastes their bandwidth)
     if (gn > 0 && gate_closed(gst, gn)) return;
     float inv[M];
 #pragma unroll
@@ -133,25 +142,6 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
             inv[m] = rsqrtf(wave_sum(ss) / (float)K + nrm.eps);
         }
     }
-    for (int c0 = w; c0 < nchunk; c0 += 4 * DEPTH) {
-#pragma unroll
-        for (int d = 0; d < DEPTH; ++d) {
-            const int c = c0 + 4 * d;
-            if (c < nchunk) {
-#pragma unroll
-                for (int r = 0; r < NR; ++r)
-#pragma unroll
-                    for (int m = 0; m < M; ++m) acc[r * M + m] = dot8(wr[d][r], xv[d][m], acc[r * M + m]);
-                if (c + 4 * DEPTH < nchunk) load(c + 4 * DEPTH, d);
-            }
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < V; ++i) {
-        const float s = wave_sum(acc[i]);
-        if (lane == 0) red[w][i] = s;
-    }
-    __syncthreads();
     // row sums (NORMP: times the row's inv — the folded RMSNorm; 1 otherwise)
     auto invm = [&](int m) {  // select chain: a runtime index into inv[] would put it in scratch
         float v = inv[0];
@@ -160,85 +150,118 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
         return v;
     };
     auto tot = [&](int i) { return (red[0][i] + red[1][i] + red[2][i] + red[3][i]) * invm(i % M); };
-    if constexpr (ROPE) {
-        // thread t < RP*M: pair (r, r+RP) of row m; the unfused path rounds the GEMM output to bf16 before RoPE
-        const int t = threadIdx.x;
-        if (t >= RP * M) return;
-        const int pr = t / M, m = t % M;
-        if (m >= mrows) return;
-        const int unit = blockIdx.x / RWG, d = RP * (blockIdx.x % RWG) + pr;  // head (q | k | v), dim in [0, 64)
-        const float x1 = bf2f(f2bf(tot(pr * M + m))), x2 = bf2f(f2bf(tot((pr + RP) * M + m)));
-        const int p = rp.pos[m];
-        const int64_t blk = rp.bt[(int64_t)rp.tok_seq[m] * rp.bt_stride + p / rp.bs];
-        const int off = p % rp.bs;
-        if (unit < rp.hq + rp.hkv) {
-            const float c = rp.cos_sin[(int64_t)p * 128 + d], sn = rp.cos_sin[(int64_t)p * 128 + 64 + d];
-            const float fa = x1 * c - x2 * sn, fb = x2 * c + x1 * sn;
-            if (unit < rp.hq) {
-                uint16_t* dst = rp.q_out + ((int64_t)m * rp.hq + unit) * 128;
-                dst[d] = f2bf(fa);
-                dst[64 + d] = f2bf(fb);
-            } else if constexpr (MODE == kRope8) {
-                uint8_t* dst = reinterpret_cast<uint8_t*>(rp.kc) + ((blk * rp.hkv + (unit - rp.hq)) * rp.bs + off) * 128;
-                const uint32_t q = f32x4_to_fp8x4(fa * rp.k_inv, fb * rp.k_inv, 0.f, 0.f);
-                dst[d] = (uint8_t)q;
-                dst[64 + d] = (uint8_t)(q >> 8);
-            } else {
-                uint16_t* dst = reinterpret_cast<uint16_t*>(rp.kc) + ((blk * rp.hkv + (unit - rp.hq)) * rp.bs + off) * 128;
-                dst[d] = f2bf(fa);
-                dst[64 + d] = f2bf(fb);
-            }
-        } else {  // v: transposed [blk, h, dim, slot]
-            const int64_t base = ((blk * rp.hkv + (unit - rp.hq - rp.hkv)) * 128) * (int64_t)rp.bs + off;
-            if constexpr (MODE == kRope8) {
-                uint8_t* dst = reinterpret_cast<uint8_t*>(rp.vc) + base;
-                const uint32_t q = f32x4_to_fp8x4(x1 * rp.v_inv, x2 * rp.v_inv, 0.f, 0.f);
-                dst[(int64_t)d * rp.bs] = (uint8_t)q;
-                dst[(int64_t)(64 + d) * rp.bs] = (uint8_t)(q >> 8);
-            } else {
-                uint16_t* dst = reinterpret_cast<uint16_t*>(rp.vc) + base;
-                dst[(int64_t)d * rp.bs] = f2bf(x1);
-                dst[(int64_t)(64 + d) * rp.bs] = f2bf(x2);
+    while (true) {
+        float acc[V];
+#pragma unroll
+        for (int i = 0; i < V; ++i) acc[i] = 0.f;
+        for (int c0 = w; c0 < nchunk; c0 += 4 * DEPTH) {
+#pragma unroll
+            for (int d = 0; d < DEPTH; ++d) {
+                const int c = c0 + 4 * d;
+                if (c < nchunk) {
+#pragma unroll
+                    for (int r = 0; r < NR; ++r)
+#pragma unroll
+                        for (int m = 0; m < M; ++m) acc[r * M + m] = dot8(wr[d][r], xv[d][m], acc[r * M + m]);
+                    if (c + 4 * DEPTH < nchunk) load(c + 4 * DEPTH, d);
+                }
             }
         }
-        return;
-    }
-    if constexpr (MODE == kResid) {
-        // s = bf16(bf16(y) + r) -> rout; per-row sum of s^2 over this workgroup's R outputs -> part_out (fixed order)
-        __shared__ float sq[R * M];
-        const int t = threadIdx.x;
-        if (t < R * M) {
-            const int r = t / M, m = t % M;
-            float v = 0.f;
-            if (m < mrows) {
-                const int64_t i = (int64_t)m * nout + n0 + r;
-                const uint16_t sb = f2bf(bf2f(f2bf(tot(t))) + bf2f(nrm.rin[i]));
-                nrm.rout[i] = sb;
-                v = bf2f(sb) * bf2f(sb);
-            }
-            sq[t] = v;
+        const int bid = g, n0 = g * R;
+        g += gridDim.x;
+        const bool more = g < ngroups;
+        if (more) {  // the ring is consumed: start the next group's weight stream before this group's epilogue
+            set_rows(g);
+            prologue();
+        }
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            const float s = wave_sum(acc[i]);
+            if (lane == 0) red[w][i] = s;
         }
         __syncthreads();
-        if (t < M && t < mrows) {
-            float ss = 0.f;
+        if constexpr (ROPE) {
+            // thread t < RP*M: pair (r, r+RP) of row m; the unfused path rounds the GEMM output to bf16 before RoPE
+            const int t = threadIdx.x;
+            const int pr = t / M, m = t % M;
+            if (t < RP * M && m < mrows) {
+                const int unit = bid / RWG, d = RP * (bid % RWG) + pr;  // head (q | k | v), dim in [0, 64)
+                const float x1 = bf2f(f2bf(tot(pr * M + m))), x2 = bf2f(f2bf(tot((pr + RP) * M + m)));
+                const int p = rp.pos[m];
+                const int64_t blk = rp.bt[(int64_t)rp.tok_seq[m] * rp.bt_stride + p / rp.bs];
+                const int off = p % rp.bs;
+                if (unit < rp.hq + rp.hkv) {
+                    const float c = rp.cos_sin[(int64_t)p * 128 + d], sn = rp.cos_sin[(int64_t)p * 128 + 64 + d];
+                    const float fa = x1 * c - x2 * sn, fb = x2 * c + x1 * sn;
+                    if (unit < rp.hq) {
+                        uint16_t* dst = rp.q_out + ((int64_t)m * rp.hq + unit) * 128;
+                        dst[d] = f2bf(fa);
+                        dst[64 + d] = f2bf(fb);
+                    } else if constexpr (MODE == kRope8) {
+                        uint8_t* dst =
+                            reinterpret_cast<uint8_t*>(rp.kc) + ((blk * rp.hkv + (unit - rp.hq)) * rp.bs + off) * 128;
+                        const uint32_t q = f32x4_to_fp8x4(fa * rp.k_inv, fb * rp.k_inv, 0.f, 0.f);
+                        dst[d] = (uint8_t)q;
+                        dst[64 + d] = (uint8_t)(q >> 8);
+                    } else {
+                        uint16_t* dst =
+                            reinterpret_cast<uint16_t*>(rp.kc) + ((blk * rp.hkv + (unit - rp.hq)) * rp.bs + off) * 128;
+                        dst[d] = f2bf(fa);
+                        dst[64 + d] = f2bf(fb);
+                    }
+                } else {  // v: transposed [blk, h, dim, slot]
+                    const int64_t base = ((blk * rp.hkv + (unit - rp.hq - rp.hkv)) * 128) * (int64_t)rp.bs + off;
+                    if constexpr (MODE == kRope8) {
+                        uint8_t* dst = reinterpret_cast<uint8_t*>(rp.vc) + base;
+                        const uint32_t q = f32x4_to_fp8x4(x1 * rp.v_inv, x2 * rp.v_inv, 0.f, 0.f);
+                        dst[(int64_t)d * rp.bs] = (uint8_t)q;
+                        dst[(int64_t)(64 + d) * rp.bs] = (uint8_t)(q >> 8);
+                    } else {
+                        uint16_t* dst = reinterpret_cast<uint16_t*>(rp.vc) + base;
+                        dst[(int64_t)d * rp.bs] = f2bf(x1);
+                        dst[(int64_t)(64 + d) * rp.bs] = f2bf(x2);
+                    }
+                }
+            }
+        } else if constexpr (MODE == kResid) {
+            // s = bf16(bf16(y) + r) -> rout; per-row sum of s^2 over this group's R outputs -> part_out (fixed order)
+            __shared__ float sq[R * M];
+            const int t = threadIdx.x;
+            if (t < R * M) {
+                const int r = t / M, m = t % M;
+                float v = 0.f;
+                if (m < mrows) {
+                    const int64_t i = (int64_t)m * nout + n0 + r;
+                    const uint16_t sb = f2bf(bf2f(f2bf(tot(t))) + bf2f(nrm.rin[i]));
+                    nrm.rout[i] = sb;
+                    v = bf2f(sb) * bf2f(sb);
+                }
+                sq[t] = v;
+            }
+            __syncthreads();
+            if (t < M && t < mrows) {
+                float ss = 0.f;
 #pragma unroll
-            for (int r = 0; r < R; ++r) ss += sq[r * M + t];
-            nrm.part_out[t * gridDim.x + blockIdx.x] = ss;
-        }
-        return;
-    }
-    for (int t = threadIdx.x; t < R * M; t += 256) {
-        const int r = t / M, m = t % M;
-        if (m >= mrows) continue;
-        const float g = tot(r * M + m);
-        if constexpr (SWIGLU) {
-            const float u = tot((R + r) * M + m);
-            const float gb = bf2f(f2bf(g)), ub = bf2f(f2bf(u));  // the unfused path rounds the GEMM outputs
-            const float sg = bf2f(f2bf(gb / (1.f + __expf(-gb))));
-            y[(int64_t)m * nout + n0 + r] = f2bf(sg * ub);
+                for (int r = 0; r < R; ++r) ss += sq[r * M + t];
+                nrm.part_out[t * ngroups + bid] = ss;
+            }
         } else {
-            y[(int64_t)m * nout + n0 + r] = f2bf(g);
+            for (int t = threadIdx.x; t < R * M; t += 256) {
+                const int r = t / M, m = t % M;
+                if (m >= mrows) continue;
+                const float gv = tot(r * M + m);
+                if constexpr (SWIGLU) {
+                    const float u = tot((R + r) * M + m);
+                    const float gb = bf2f(f2bf(gv)), ub = bf2f(f2bf(u));  // the unfused path rounds the GEMM outputs
+                    const float sg = bf2f(f2bf(gb / (1.f + __expf(-gb))));
+                    y[(int64_t)m * nout + n0 + r] = f2bf(sg * ub);
+                } else {
+                    y[(int64_t)m * nout + n0 + r] = f2bf(gv);
+                }
+            }
         }
+        if (!more) break;
+        __syncthreads();  // red / sq are rewritten by the next group
     }
 }
 
@@ -283,9 +306,13 @@ static void launch_m(const uint16_t* x, int mrows, int K, const uint16_t* W, int
     // costs 0.28 ms instead of 2.25 (the late check let every workgroup issue its first ring of weight loads, which
     // at K = 4096 is the whole row), and the live step is no slower (3.60 vs 3.72 ms/token; profiles/r2_studies.md)
     const int gn = gst ? (knob("gemv_early_gate", 1) ? -g_gate_n : g_gate_n) : 0;
+    // At most `persist` workgroups, each looping over row groups with the next group's weight ring prefetched: 512
+    // (two per CU) measured 2.88 ms/token in the single-stream decode step against 3.06 with one workgroup per group
+    // (256: 3.55, 384: 3.10, 640: 3.17, 1024: 2.95; profiles/r2_single_stream_gemv_persist_ab.json).  0 = one per group.
+    const int persist = knob("gemv_persist", 512);
 #define GV(MODE_, NP_, RR, GRID, NOUT, HALF)                                                                     \
-    hipLaunchKernelGGL((gemv_kernel<M, RR, MODE_, NP_>), dim3(GRID), dim3(256), 0, st, x, mrows, K, W, y, NOUT, \
-                       HALF, na, ra, gst, gn)
+    hipLaunchKernelGGL((gemv_kernel<M, RR, MODE_, NP_>), dim3(persist > 0 && persist < (GRID) ? persist : (GRID)), \
+                       dim3(256), 0, st, x, mrows, K, W, y, NOUT, HALF, na, ra, gst, gn, (GRID))
     if (mode == kSwiglu) {
         const int F = N / 2;
         if constexpr (M == 1) {

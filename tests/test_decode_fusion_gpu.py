@@ -24,6 +24,15 @@ def _lib():
     assert "_C" in n._loaded, "HIP kernel library must be the one running"
 
 
+@pytest.fixture(params=[0, 37], ids=["grid", "persist37"])
+def persist(request):
+    """gemv.hip knob gemv_persist: 0 = one workgroup per row group; 37 = a 37-workgroup grid looping over the groups
+    with the next group's weight ring prefetched (uneven: some workgroups get one group more)."""
+    torch.ops.chronos.set_knob("gemv_persist", request.param)
+    yield request.param
+    torch.ops.chronos.set_knob("gemv_persist", -1)
+
+
 def _rand(g, *shape, scale=1.0):
     return (torch.randn(*shape, device=DEV, generator=g) * scale).to(torch.bfloat16)
 
@@ -35,7 +44,7 @@ def _close(a, b, atol, rtol):
 
 @pytest.mark.parametrize("m", [1, 2])
 @pytest.mark.parametrize("n_out", [4096, 8192])
-def test_gemv_resid_producer(m, n_out):
+def test_gemv_resid_producer(m, n_out, persist):
     """resid_out = bf16(bf16(x W^T) + resid) bit-exact vs GEMV + add; partials sum to sum(resid_out^2)."""
     from chronos import ops
     from chronos.ops import gemm
@@ -55,7 +64,7 @@ def test_gemv_resid_producer(m, n_out):
 
 @pytest.mark.parametrize("m", [1, 2])
 @pytest.mark.parametrize("swiglu,n", [(False, 6144), (True, 2 * 1792)])
-def test_gemv_normp_consumer(m, swiglu, n):
+def test_gemv_normp_consumer(m, swiglu, n, persist):
     """The folded norm (norm weight inside W, inv from the producer's partials) equals the standalone RMSNorm -> GEMV
     on the unfolded weights, to bf16 rounding; and it is deterministic."""
     from chronos import ops
@@ -83,7 +92,7 @@ def test_gemv_normp_consumer(m, swiglu, n):
 @pytest.mark.parametrize("fp8", [False, True])
 @pytest.mark.parametrize("m,hq,hkv", [(1, 32, 8), (2, 32, 8), (1, 8, 1)])
 @pytest.mark.parametrize("folded", [False, True])
-def test_qkv_rope_equals_unfused(fp8, m, hq, hkv, folded):
+def test_qkv_rope_equals_unfused(fp8, m, hq, hkv, folded, persist):
     """QKV GEMV + RoPE/paged-KV epilogue == GEMV then rope_kv_write (bit-exact on a plain input; with the folded norm
     — norm weight inside W, inv from partials — against the standalone-norm chain, to bf16 rounding)."""
     from chronos import ops
@@ -136,7 +145,7 @@ def test_qkv_rope_equals_unfused(fp8, m, hq, hkv, folded):
         assert torch.equal(vc, vc2)
 
 
-def test_decode_gate_skips_finished_steps():
+def test_decode_gate_skips_finished_steps(persist):
     """Armed on a state vector with no live row, in-place kernels (residual norm, fused QKV + KV write) leave their
     outputs untouched; one live row and they run again."""
     from chronos import ops
