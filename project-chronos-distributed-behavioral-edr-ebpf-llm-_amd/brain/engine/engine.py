@@ -83,7 +83,10 @@ class EngineConfig:
     prefill_ramp: int = 2048
     # Jump-forward over grammar-forced token runs (brain/constrain GrammarBank.jumps) while at most jump_max_rows
     # sequences decode: a row entering a forced run parks, and the host appends the run in one prefill-mode forward
-    # instead of one decode step per token.  Larger decode batches are compute-bound, where it would not pay.
+    # instead of one decode step per token.  Larger decode batches are compute-bound, where it would not pay.  The
+    # forced run's token ids are its canonical tokenization, so a request's token ids (never the text of the forced
+    # runs) can differ between a small batch and a large one; the GPU's batch-size-dependent GEMM kernels already make
+    # outputs batch-dependent in the same way.
     jump_forward: bool = True
     jump_max_rows: int = 8
     # token automata compiled at start-up (a first request must not pay the ~4 s vocab walk: the reference's cold-start
