@@ -16,10 +16,14 @@ Routing is by measured shape (profiles/r1_gemm_vs_hipblaslt.json, cold weights, 
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Callable, Optional
 
 import torch
+
+# Largest M routed to the GEMV (gemv_ok).  Env CHRONOS_GEMV_MAX_M; scripts/single_stream.py A/Bs it (py_gemv_max_m).
+GEMV_MAX_M = int(os.environ.get("CHRONOS_GEMV_MAX_M", "2"))
 
 # (M, N, K) -> bool predicate + kernel; extension point for further shape-specialised kernels
 _custom: list[tuple[Callable[[int, int, int], bool], Callable[[torch.Tensor, torch.Tensor], torch.Tensor]]] = []
@@ -93,7 +97,7 @@ def gemv_ok(m: int, n: int, k: int, swiglu: bool = False) -> bool:
     beats hipBLASLt on cold weights (profiles/r1_kernels.json): M == 1 always, M == 2 below LM-head widths."""
     if k % 512 or n % 16:
         return False
-    return m == 1 or (m == 2 and n <= 32768)
+    return m == 1 or (m <= GEMV_MAX_M and n <= 32768)
 
 
 def mfma_swiglu_ok(m: int, n: int, k: int) -> bool:

@@ -61,7 +61,7 @@ def main():
         for k, v in knobsets.get(name, {}).items():
             if k == "py_split_max":  # decode kv-split cap (ops.pick_nsplit), baked into the captured graph
                 ops._SPLIT_MAX = v
-            elif k in ("py_burst", "py_jump"):  # engine decode_burst / jump_forward
+            elif k in ("py_burst", "py_jump", "py_gemv_max_m"):  # engine decode_burst / jump_forward / GEMV routing
                 pass
             else:
                 torch.ops.chronos.set_knob(k, v)  # read when this engine's decode graph is captured
@@ -82,9 +82,13 @@ def main():
     for eng, _ in engines.values():
         eng.phase_s.clear()
         eng.stats.clear()
+    from chronos.ops import gemm
+
+    gemv_m0 = gemm.GEMV_MAX_M
     for p in prompts[1:]:
         for name, (eng, fuse) in engines.items():
             llama._FUSE_NORM = fuse
+            gemm.GEMV_MAX_M = knobsets.get(name, {}).get("py_gemv_max_m", gemv_m0)  # eager (jump) forwards
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             r = eng.submit(p, fmt=VERDICT_SCHEMA, num_predict=a.num_predict)
