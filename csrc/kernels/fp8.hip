@@ -308,30 +308,33 @@ __device__ __forceinline__ float qdot16(const u8x16& wq, const bf16x2_t (&xb)[8]
     return acc;
 }
 
+// Like gemv.hip's gemv_kernel: a grid of at most `gemv_persist` workgroups loops over the row groups (R rows each),
+// issuing the next group's weight ring as soon as the current group's dot products have consumed it.
 template <int M, int R, bool SWIGLU>
 __global__ void __launch_bounds__(256) qgemv_kernel(const uint8_t* __restrict__ x, const float* __restrict__ xs,
                                                     int mrows, int K, const uint8_t* __restrict__ W,
                                                     const float* __restrict__ ws, uint16_t* __restrict__ y, int nout,
-                                                    int half) {
+                                                    int half, const int32_t* __restrict__ gst, int gn, int ngroups) {
+    if (gate_closed(gst, gn)) return;  // decode early-exit gate, read before any weight load (chronos_hip.h)
+    int g = blockIdx.x;
+    if (g >= ngroups) return;
     constexpr int NR = SWIGLU ? 2 * R : R;
     constexpr int V = NR * M;
     constexpr int DEPTH = (NR + M) * 4 <= 40 ? 3 : 2;
     __shared__ float red[4][V];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int n0 = blockIdx.x * R;
     const int nchunk = K >> 10;  // 1024-byte chunks per row
     const u8x16* wrow[NR];
+    auto set_rows = [&](int bid) {
+        const int n0 = bid * R;
 #pragma unroll
-    for (int r = 0; r < NR; ++r) {
-        const int row = (SWIGLU && r >= R) ? half + n0 + (r - R) : n0 + r;
-        wrow[r] = reinterpret_cast<const u8x16*>(W + (int64_t)row * K);
-    }
+        for (int r = 0; r < NR; ++r) {
+            const int row = (SWIGLU && r >= R) ? half + n0 + (r - R) : n0 + r;
+            wrow[r] = reinterpret_cast<const u8x16*>(W + (int64_t)row * K);
+        }
+    };
     const u8x16* xr = reinterpret_cast<const u8x16*>(x);
     const int xstride = K >> 4;
-
-    float acc[V];
-#pragma unroll
-    for (int i = 0; i < V; ++i) acc[i] = 0.f;
     u8x16 wr[DEPTH][NR], xv[DEPTH][M];
     auto load = [&](int c, u8x16 (&wd)[NR], u8x16 (&xd)[M]) {
         const int off = c * 64 + lane;
@@ -340,50 +343,68 @@ __global__ void __launch_bounds__(256) qgemv_kernel(const uint8_t* __restrict__ 
 #pragma unroll
         for (int m = 0; m < M; ++m) xd[m] = m < mrows ? xr[m * xstride + off] : u8x16{};
     };
+    auto prologue = [&]() {
 #pragma unroll
-    for (int d = 0; d < DEPTH; ++d)
-        if (w + 4 * d < nchunk) load(w + 4 * d, wr[d], xv[d]);
-    for (int cb = w; cb < nchunk; cb += 4 * DEPTH) {
+        for (int d = 0; d < DEPTH; ++d)
+            if (w + 4 * d < nchunk) load(w + 4 * d, wr[d], xv[d]);
+    };
+    set_rows(g);
+    prologue();
+    while (true) {
+        float acc[V];
 #pragma unroll
-        for (int d = 0; d < DEPTH; ++d) {
-            const int c = cb + 4 * d;
-            if (c < nchunk) {
+        for (int i = 0; i < V; ++i) acc[i] = 0.f;
+        for (int cb = w; cb < nchunk; cb += 4 * DEPTH) {
 #pragma unroll
-                for (int m = 0; m < M; ++m) {
-                    bf16x2_t xb[8];
-                    const i32x4 xi = __builtin_bit_cast(i32x4, xv[d][m]);
+            for (int d = 0; d < DEPTH; ++d) {
+                const int c = cb + 4 * d;
+                if (c < nchunk) {
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        xb[2 * j] = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(xi[j], 1.f, false);
-                        xb[2 * j + 1] = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(xi[j], 1.f, true);
+                    for (int m = 0; m < M; ++m) {
+                        bf16x2_t xb[8];
+                        const i32x4 xi = __builtin_bit_cast(i32x4, xv[d][m]);
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            xb[2 * j] = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(xi[j], 1.f, false);
+                            xb[2 * j + 1] = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(xi[j], 1.f, true);
+                        }
+#pragma unroll
+                        for (int r = 0; r < NR; ++r) acc[r * M + m] = qdot16(wr[d][r], xb, acc[r * M + m]);
                     }
-#pragma unroll
-                    for (int r = 0; r < NR; ++r) acc[r * M + m] = qdot16(wr[d][r], xb, acc[r * M + m]);
+                    if (c + 4 * DEPTH < nchunk) load(c + 4 * DEPTH, wr[d], xv[d]);
                 }
-                if (c + 4 * DEPTH < nchunk) load(c + 4 * DEPTH, wr[d], xv[d]);
             }
         }
-    }
-#pragma unroll
-    for (int i = 0; i < V; ++i) {
-        const float s = wave_sum(acc[i]);
-        if (lane == 0) red[w][i] = s;
-    }
-    __syncthreads();
-    for (int t = threadIdx.x; t < R * M; t += 256) {
-        const int r = t / M, m = t % M;
-        if (m >= mrows) continue;
-        const float sxm = xs[m];
-        const float g = (red[0][r * M + m] + red[1][r * M + m] + red[2][r * M + m] + red[3][r * M + m]) * sxm *
-                        ws[n0 + r];
-        if constexpr (SWIGLU) {
-            const int ru = (R + r) * M + m;
-            const float u = (red[0][ru] + red[1][ru] + red[2][ru] + red[3][ru]) * sxm * ws[half + n0 + r];
-            const float gb = bf2f(f2bf(g)), ub = bf2f(f2bf(u));
-            y[(int64_t)m * nout + n0 + r] = f2bf(bf2f(f2bf(gb / (1.f + __expf(-gb)))) * ub);
-        } else {
-            y[(int64_t)m * nout + n0 + r] = f2bf(g);
+        const int n0 = g * R;
+        g += gridDim.x;
+        const bool more = g < ngroups;
+        if (more) {  // the ring is consumed: start the next group's weight stream before this group's epilogue
+            set_rows(g);
+            prologue();
         }
+#pragma unroll
+        for (int i = 0; i < V; ++i) {
+            const float s = wave_sum(acc[i]);
+            if (lane == 0) red[w][i] = s;
+        }
+        __syncthreads();
+        for (int t = threadIdx.x; t < R * M; t += 256) {
+            const int r = t / M, m = t % M;
+            if (m >= mrows) continue;
+            const float sxm = xs[m];
+            const float gv = (red[0][r * M + m] + red[1][r * M + m] + red[2][r * M + m] + red[3][r * M + m]) * sxm *
+                             ws[n0 + r];
+            if constexpr (SWIGLU) {
+                const int ru = (R + r) * M + m;
+                const float u = (red[0][ru] + red[1][ru] + red[2][ru] + red[3][ru]) * sxm * ws[half + n0 + r];
+                const float gb = bf2f(f2bf(gv)), ub = bf2f(f2bf(u));
+                y[(int64_t)m * nout + n0 + r] = f2bf(bf2f(f2bf(gb / (1.f + __expf(-gb)))) * ub);
+            } else {
+                y[(int64_t)m * nout + n0 + r] = f2bf(gv);
+            }
+        }
+        if (!more) break;
+        __syncthreads();  // red is rewritten by the next group
     }
 }
 
@@ -409,12 +430,15 @@ void qgemv_m(const uint8_t* x, const float* xs, int mrows, int K, const uint8_t*
              bool swiglu, hipStream_t st) {
     constexpr int R1 = M <= 2 ? 8 : 4;
     constexpr int R2 = M <= 2 ? 4 : 2;
+    const int persist = knob("gemv_persist", 512);  // as gemv.hip: 0 = one workgroup per row group
+    auto grid = [&](int groups) { return persist > 0 && persist < groups ? persist : groups; };
     if (swiglu) {
         const int F = N / 2;
-        hipLaunchKernelGGL((qgemv_kernel<M, R2, true>), dim3(F / R2), dim3(256), 0, st, x, xs, mrows, K, W, ws, y, F, F);
+        hipLaunchKernelGGL((qgemv_kernel<M, R2, true>), dim3(grid(F / R2)), dim3(256), 0, st, x, xs, mrows, K, W, ws,
+                           y, F, F, CHRONOS_GATE, F / R2);
     } else {
-        hipLaunchKernelGGL((qgemv_kernel<M, R1, false>), dim3(N / R1), dim3(256), 0, st, x, xs, mrows, K, W, ws, y, N,
-                           0);
+        hipLaunchKernelGGL((qgemv_kernel<M, R1, false>), dim3(grid(N / R1)), dim3(256), 0, st, x, xs, mrows, K, W, ws,
+                           y, N, 0, CHRONOS_GATE, N / R1);
     }
 }
 

@@ -9,7 +9,7 @@ def short(n):
     if n.startswith("Cijk") or n.startswith("Custom_Cijk"):
         return "gemm:" + n.split("_MT")[1].split("_")[0] if "_MT" in n else "gemm"
     n = n.replace("void ", "")
-    return n.split("(")[0][:60]
+    return n.replace("(anonymous namespace)::", "").split("(")[0][:60]
 
 
 rows = list(csv.DictReader(open(sys.argv[1])))

@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--only", choices=list(VARIANTS), default="fused", help="variant without --ab")
     ap.add_argument("--knob-ab", default=None,
                     help="';'-separated knob sets ('name=v,name=v'), one fused engine captured under each, interleaved")
+    ap.add_argument("--weights", choices=["bf16", "fp8"], default="bf16")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
 
@@ -68,7 +69,7 @@ def main():
         llama._FUSE_NORM = fuse
         burst = knobsets.get(name, {}).get("py_burst", a.burst)
         eng = Engine(EngineConfig(model=a.model, device="cuda", max_slots=8, max_model_len=512, decode_burst=burst,
-                                  decode_gate=gate, seed=0, async_harvest=a.async_harvest,
+                                  decode_gate=gate, seed=0, async_harvest=a.async_harvest, weight_dtype=a.weights,
                                   jump_forward=bool(knobsets.get(name, {}).get("py_jump", 1))))
         # capture the n=1 graph under this variant's setting
         eng.submit(prompts[0], fmt=VERDICT_SCHEMA, num_predict=a.num_predict)

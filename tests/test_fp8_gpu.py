@@ -86,6 +86,13 @@ def test_qlinear(m, n, k, swiglu):
     y = torch.ops.chronos.qlinear(xq, xs, wq, ws, swiglu)
     assert y.shape == yr.shape == (m, n // 2 if swiglu else n)
     torch.testing.assert_close(y.float(), yr.float(), **tol)
+    if m <= 4:  # fp8 GEMV: one workgroup per row group, and an uneven 37-workgroup loop, give the same bits
+        for persist in (0, 37):
+            torch.ops.chronos.set_knob("gemv_persist", persist)
+            try:
+                assert torch.equal(torch.ops.chronos.qlinear(xq, xs, wq, ws, swiglu), y)
+            finally:
+                torch.ops.chronos.set_knob("gemv_persist", -1)
 
 
 @pytest.mark.parametrize("tile", [128, 256])
