@@ -114,6 +114,15 @@ __device__ __forceinline__ bool gate_closed(const int32_t* st, int n) {
     return !live;
 }
 
+// Workgroups of `kernel` (block threads, no dynamic LDS) resident on the whole device at once: the occupancy
+// calculator's per-CU count times the CU count, cached per kernel (bindings.cpp).  Persistent grids are sized by it: a
+// grid larger than what fits serialises its surplus workgroups behind the first ones.
+int resident_workgroups_of(const void* kernel, int threads);
+template <typename K>
+inline int resident_workgroups(K kernel, int threads) {
+    return resident_workgroups_of(reinterpret_cast<const void*>(kernel), threads);
+}
+
 // Host-side tuning knobs (defined in bindings.cpp): value set through torch.ops.chronos.set_knob(name, v), else the
 // environment variable CHRONOS_<NAME>, else `dflt`.  Used for in-process A/B of kernel variants
 // (cdna_hip_programming.md §5.4 rule 24: interleave variants in ONE process).

@@ -63,6 +63,21 @@ std::mutex g_knob_mu;
 std::unordered_map<std::string, int> g_knobs;
 }  // namespace
 
+int resident_workgroups_of(const void* kernel, int threads) {
+    static std::mutex mu;
+    static std::unordered_map<const void*, int> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = cache.find(kernel);
+    if (it != cache.end()) return it->second;
+    int per_cu = 0, dev = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, 0);
+    const int v = per_cu > 0 && cus > 0 ? per_cu * cus : 256;
+    cache[kernel] = v;
+    return v;
+}
+
 int knob(const char* name, int dflt) {
     std::lock_guard<std::mutex> lk(g_knob_mu);
     auto it = g_knobs.find(name);

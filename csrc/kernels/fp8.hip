@@ -430,15 +430,19 @@ void qgemv_m(const uint8_t* x, const float* xs, int mrows, int K, const uint8_t*
              bool swiglu, hipStream_t st) {
     constexpr int R1 = M <= 2 ? 8 : 4;
     constexpr int R2 = M <= 2 ? 4 : 2;
-    const int persist = knob("gemv_persist", 512);  // as gemv.hip: 0 = one workgroup per row group
-    auto grid = [&](int groups) { return persist > 0 && persist < groups ? persist : groups; };
+    const int persist = knob("gemv_persist", -1);  // as gemv.hip: resident workgroups; 0 = one per row group
+    auto grid = [&](int groups, int fit) {
+        const int cap = persist == 0 ? groups : persist > 0 && persist < fit ? persist : fit;
+        return cap < groups ? cap : groups;
+    };
     if (swiglu) {
         const int F = N / 2;
-        hipLaunchKernelGGL((qgemv_kernel<M, R2, true>), dim3(grid(F / R2)), dim3(256), 0, st, x, xs, mrows, K, W, ws,
-                           y, F, F, CHRONOS_GATE, F / R2);
+        hipLaunchKernelGGL((qgemv_kernel<M, R2, true>), dim3(grid(F / R2, resident_workgroups(qgemv_kernel<M, R2, true>, 256))),
+                           dim3(256), 0, st, x, xs, mrows, K, W, ws, y, F, F, CHRONOS_GATE, F / R2);
     } else {
-        hipLaunchKernelGGL((qgemv_kernel<M, R1, false>), dim3(grid(N / R1)), dim3(256), 0, st, x, xs, mrows, K, W, ws,
-                           y, N, 0, CHRONOS_GATE, N / R1);
+        hipLaunchKernelGGL((qgemv_kernel<M, R1, false>),
+                           dim3(grid(N / R1, resident_workgroups(qgemv_kernel<M, R1, false>, 256))), dim3(256), 0, st,
+                           x, xs, mrows, K, W, ws, y, N, 0, CHRONOS_GATE, N / R1);
     }
 }
 

@@ -73,7 +73,8 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
     constexpr int NPQ = M == 1 ? 8 : 4;  // NORMP: float4 partials per lane (<= 2048 / 1024 per row)
     constexpr int NR = SWIGLU ? 2 * R : R;  // weight rows streamed per group
     constexpr int V = NR * M;               // partial sums per lane
-    constexpr int DEPTH = (NR + M) * 4 <= 40 ? 3 : 2;  // register ring depth (VGPR budget)
+    // register ring depth (VGPR budget): M = 2 with 8 rows at depth 3 took all 256 VGPRs (one wave per SIMD)
+    constexpr int DEPTH = (NR + M) * 4 < 40 ? 3 : 2;
     // gn < 0: check the decode gate BEFORE the first weight loads (a closed gate then streams no weights; an open one
     // pays the state read's latency up front).  gn > 0: after them (below).
     if (gn < 0 && gate_closed(gst, -gn)) return;
@@ -306,13 +307,19 @@ static void launch_m(const uint16_t* x, int mrows, int K, const uint16_t* W, int
     // costs 0.28 ms instead of 2.25 (the late check let every workgroup issue its first ring of weight loads, which
     // at K = 4096 is the whole row), and the live step is no slower (3.60 vs 3.72 ms/token; profiles/r2_studies.md)
     const int gn = gst ? (knob("gemv_early_gate", 1) ? -g_gate_n : g_gate_n) : 0;
-    // At most `persist` workgroups, each looping over row groups with the next group's weight ring prefetched: 512
-    // (two per CU) measured 2.88 ms/token in the single-stream decode step against 3.06 with one workgroup per group
-    // (256: 3.55, 384: 3.10, 640: 3.17, 1024: 2.95; profiles/r2_single_stream_gemv_persist_ab.json).  0 = one per group.
-    const int persist = knob("gemv_persist", 512);
+    // Persistent grid: the workgroups that fit on the device at once (occupancy x CUs), each looping over row groups
+    // with the next group's weight ring prefetched.  A grid of 512 for every kernel (two per CU, what the 2-wave
+    // gate_up fits) measured 2.88 ms/token in the single-stream decode step against 3.06 with one workgroup per group
+    // (256: 3.55, 384: 3.10, 640: 3.17, 1024: 2.95 — counts beyond what fits serialise; profiles/
+    // r2_single_stream_gemv_persist_ab.json).  Knob gemv_persist: 0 = one workgroup per group, N > 0 = at most N.
+    const int persist = knob("gemv_persist", -1);
 #define GV(MODE_, NP_, RR, GRID, NOUT, HALF)                                                                     \
-    hipLaunchKernelGGL((gemv_kernel<M, RR, MODE_, NP_>), dim3(persist > 0 && persist < (GRID) ? persist : (GRID)), \
-                       dim3(256), 0, st, x, mrows, K, W, y, NOUT, HALF, na, ra, gst, gn, (GRID))
+    do {                                                                                                         \
+        const int fit_ = resident_workgroups(gemv_kernel<M, RR, MODE_, NP_>, 256);                              \
+        const int cap_ = persist == 0 ? (GRID) : persist > 0 && persist < fit_ ? persist : fit_;                 \
+        hipLaunchKernelGGL((gemv_kernel<M, RR, MODE_, NP_>), dim3(cap_ < (GRID) ? cap_ : (GRID)), dim3(256), 0,  \
+                           st, x, mrows, K, W, y, NOUT, HALF, na, ra, gst, gn, (GRID));                          \
+    } while (0)
     if (mode == kSwiglu) {
         const int F = N / 2;
         if constexpr (M == 1) {
