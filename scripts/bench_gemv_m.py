@@ -23,11 +23,14 @@ def main():
     for name, (n, k, sw) in shapes.items():
         copies = max(2, int(1.2e9 // (n * k * 2)))
         ws = [torch.randn(n, k, device="cuda").to(torch.bfloat16) * 0.02 for _ in range(copies)]
-        for m in (1, 2, 4, 8):
+        for m in [int(v) for v in os.environ.get("MS", "1,2,4,8").split(",")]:
             x = torch.randn(m, k, device="cuda").to(torch.bfloat16)
-            for impl in ("gemv", "hipblaslt"):
+            impls = ["gemv", "hipblaslt"] + [f"gemv_persist={p}" for p in os.environ.get("PERSIST", "").split(",") if p]
+            for impl in impls:
+                if impl.startswith("gemv_persist="):
+                    torch.ops.chronos.set_knob("gemv_persist", int(impl.split("=")[1]))
                 def run(w):
-                    if impl == "gemv":
+                    if impl.startswith("gemv"):
                         return gemm._gemv(x, w, sw)
                     y = torch.matmul(x, w.t())
                     return ops.silu_mul(y) if sw else y
@@ -43,6 +46,7 @@ def main():
                 b.synchronize()
                 us = 1e3 * a.elapsed_time(b) / reps
                 out[f"{name} M={m} {impl}"] = {"us": round(us, 2), "TB/s": round(n * k * 2 / us / 1e6, 2)}
+                torch.ops.chronos.set_knob("gemv_persist", -1)
         del ws
     print(json.dumps(out))
 
