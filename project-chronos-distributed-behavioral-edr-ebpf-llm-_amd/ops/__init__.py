@@ -244,7 +244,9 @@ def attention_tiles(q_lens: list[int], hq: int, hkv: int, nqt: int) -> list[tupl
     return out
 
 
-_SPLIT_WGS = int(os.environ.get("CHRONOS_DECODE_SPLIT_WGS", "2"))   # target workgroups per CU
+# target split-K decode workgroups per CU: 1 measured best at every long-context shape (profiles/r2_attn_nsplit_sweep.json:
+# 1 x 128k 150 -> 125 us per layer (64 -> 32 splits), 4 x 32k 113 -> 110, 16 x 8k 117 -> 113); 2 over-splits
+_SPLIT_WGS = int(os.environ.get("CHRONOS_DECODE_SPLIT_WGS", "1"))
 _SPLIT_MAX = int(os.environ.get("CHRONOS_DECODE_SPLIT_MAX", "64"))
 
 

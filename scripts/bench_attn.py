@@ -78,10 +78,13 @@ def main():
         ns = ops.pick_nsplit(B * hkv, ctx)
         res = {}
         outs = {}
-        for name, kn in variants.items():
+        runs = [(name, kn, ns) for name, kn in variants.items()]
+        if os.environ.get("ATTN_NSPLITS"):  # the split count itself (default kernel knobs)
+            runs = [(f"nsplit{n}", {}, int(n)) for n in os.environ["ATTN_NSPLITS"].split(",")]
+        for name, kn, nsp in runs:
             for kk, vv in kn.items():
                 C.set_knob(kk, vv)
-            fn = lambda: ops.paged_attention(q, k, v, bt, qs, cl, None, B, 1, ns)  # noqa: E731
+            fn = lambda: ops.paged_attention(q, k, v, bt, qs, cl, None, B, 1, nsp)  # noqa: E731
             outs[name] = fn().float()
             res[name] = timeit(fn)
         ref = outs[next(iter(outs))]

@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--device", default="cuda")
     ap.add_argument("--cp", type=int, default=1, help="context-parallel ranks (torch.distributed.run)")
     ap.add_argument("--repeat", type=int, default=1, help="run the long request this many times (first = cold)")
+    ap.add_argument("--no-jump-forward", action="store_true")
     a = ap.parse_args()
     from chronos.brain.engine.engine import Engine, EngineConfig
     from chronos.parallel.tp import TPContext
@@ -56,7 +57,8 @@ def main():
 
     eng = Engine(EngineConfig(model=a.model, device=a.device, max_slots=1, max_model_len=131072,
                               max_prefill_tokens=a.chunk, kv_dtype=a.kv_dtype, decode_burst=8, prefix_cache=False,
-                              cp_min_tokens=min(4096, a.chunk), weight_dtype=a.weights),
+                              cp_min_tokens=min(4096, a.chunk), weight_dtype=a.weights,
+                              jump_forward=not a.no_jump_forward),
                  cp=cp)
     # a very long chain: concatenated fleet histories (one process tree that never triggered a reset)
     hist = []
