@@ -20,6 +20,19 @@
 //               peer buffers, sums in fp32, writes bf16 output.
 // Memory ordering follows MI355X_MICROARCH.md's cross-agent hand-off table: release by the storing side before the
 // flag, acquire by the polling side before the data loads.
+//
+// Two-shot variant (mid-sized messages, e.g. 70B TP8 decode at B >= 64: 1-8 MiB).  One-shot reads W full copies
+// per rank, so above ~1 MiB it is bound by the W-fold xGMI reads.  Two-shot splits the message into W slices, rank r
+// owning slice r: (A) publish all slices as above; (B) reduce-scatter: rank r reads slice r from every peer, sums,
+// writes it to its output and back over slice r of its own exchange buffer, then raises a second flag;
+// (C) all-gather: after every peer's second flag, rank r reads slice p from peer p's buffer.  Each rank reads
+// 2(W-1)/W of the message over xGMI instead of (W-1), in two dependent hops instead of one.
+// Flag values: phase A of call e stores 2e-1, phase B stores 2e, so one flag array serves both kernels and the
+// values stay monotonic whichever kernel each call uses (waits are "flag - target >= 0").
+// Overwriting slice r in place is safe: in phase B peers only read their own slice p != r of my buffer, and slice r
+// of my buffer is read by peers only after my phase-B flag.  A peer still gathering from call e-2 (same parity half)
+// cannot exist: my call e started after my call e-1 saw that peer's phase-B flag of call e-1, which the peer raised
+// after its call e-2 kernel had finished (stream order).
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstring>
@@ -39,6 +52,43 @@ struct ArPeers {
     uint16_t* data[kArMaxWorld];   // each rank's data buffer (2 halves of half_elems bf16), mapped into this process
     uint32_t* flags[kArMaxWorld];  // each rank's flag array [kArMaxWorld src][kArMaxBlocks], mapped
 };
+
+// One thread: wait until every peer's flag for block b has reached target (bounded spin; a lost peer sets the error
+// word and returns 0 instead of hanging the GPU).
+__device__ int ar_wait_peers(const ArPeers& peers, int rank, int world, int b, uint32_t target, uint32_t* ctl,
+                             int64_t spin_limit) {
+    for (int p = 0; p < world; ++p) {
+        const uint32_t* f = &peers.flags[rank][p * kArMaxBlocks + b];
+        int64_t spins = 0;
+        while ((int32_t)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - target) < 0) {
+            if (++spins > spin_limit) {
+                __hip_atomic_store(&ctl[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                return 0;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    return 1;
+}
+
+// One thread: release this block's stores to other agents, then raise flag value v in every peer's array.
+__device__ void ar_signal_peers(const ArPeers& peers, int rank, int world, int b, uint32_t v) {
+    __atomic_thread_fence(__ATOMIC_RELEASE);  // system scope: write back this GPU's L2 before the flag
+    for (int p = 0; p < world; ++p)
+        __hip_atomic_store(&peers.flags[p][rank * kArMaxBlocks + b], v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The last block of a call to finish advances the epoch (every block read it at its start).
+__device__ void ar_finish_call(uint32_t* ctl, uint32_t e, int nb) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t done = __hip_atomic_fetch_add(&ctl[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (done == (uint32_t)nb - 1) {
+            __hip_atomic_store(&ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&ctl[0], e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
 
 // local (non-shared) control words: [0] epoch, [1] finished-block counter, [2] error
 __global__ void __launch_bounds__(kArThreads) allreduce_kernel(ArPeers peers, const uint16_t* __restrict__ in,
@@ -63,25 +113,8 @@ __global__ void __launch_bounds__(kArThreads) allreduce_kernel(ArPeers peers, co
     __builtin_amdgcn_s_waitcnt(0);  // every thread's stores issued and retired before the block barrier
     __syncthreads();
     if (threadIdx.x == 0) {
-        __atomic_thread_fence(__ATOMIC_RELEASE);  // system scope: make the data visible to other agents
-        for (int p = 0; p < world; ++p)
-            __hip_atomic_store(&peers.flags[p][rank * kArMaxBlocks + b], e, __ATOMIC_RELEASE,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
-        // ---- wait for every peer's chunk b
-        int ok = 1;
-        for (int p = 0; p < world && ok; ++p) {
-            const uint32_t* f = &peers.flags[rank][p * kArMaxBlocks + b];
-            int64_t spins = 0;
-            while ((int32_t)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
-                if (++spins > spin_limit) {
-                    ok = 0;
-                    __hip_atomic_store(&ctl[2], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-        }
-        s_ok = ok;
+        ar_signal_peers(peers, rank, world, b, 2 * e - 1);
+        s_ok = ar_wait_peers(peers, rank, world, b, 2 * e - 1, ctl, spin_limit);  // every peer's chunk b
     }
     __syncthreads();
     if (s_ok) {
@@ -100,15 +133,74 @@ __global__ void __launch_bounds__(kArThreads) allreduce_kernel(ArPeers peers, co
             reinterpret_cast<u16x8*>(out)[v] = o;
         }
     }
-    // ---- the last block of this call advances the epoch (all blocks read it above)
+    ar_finish_call(ctl, e, nb);
+}
+
+// Two-shot: n % (8 * world) == 0 (checked on the host).  Slice r = vectors [r * sv, (r + 1) * sv); block b owns
+// sub-chunk b of every slice.
+__global__ void __launch_bounds__(kArThreads) allreduce2_kernel(ArPeers peers, const uint16_t* __restrict__ in,
+                                                                uint16_t* __restrict__ out, int64_t n,
+                                                                int64_t half_elems, int rank, int world,
+                                                                uint32_t* __restrict__ ctl, int64_t spin_limit) {
+    __shared__ uint32_t s_epoch;
+    __shared__ int s_ok;
+    const int b = blockIdx.x, nb = gridDim.x;
+    if (threadIdx.x == 0) s_epoch = __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+    __syncthreads();
+    const uint32_t e = s_epoch;
+    const int64_t sv = n / 8 / world;  // vectors per slice
+    const int64_t per = (sv + nb - 1) / nb;
+    const int64_t c0 = (int64_t)b * per, c1 = c0 + per < sv ? c0 + per : sv;
+    const int64_t half = (int64_t)(e & 1) * half_elems;
+    u16x8* mine = reinterpret_cast<u16x8*>(peers.data[rank] + half);
+    const u16x8* src = reinterpret_cast<const u16x8*>(in);
+    u16x8* dst = reinterpret_cast<u16x8*>(out);
+
+    // ---- (A) publish sub-chunk b of every slice
+    for (int s = 0; s < world; ++s)
+        for (int64_t v = s * sv + c0 + threadIdx.x; v < s * sv + c1; v += kArThreads) mine[v] = src[v];
+    __builtin_amdgcn_s_waitcnt(0);
     __syncthreads();
     if (threadIdx.x == 0) {
-        const uint32_t done = __hip_atomic_fetch_add(&ctl[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (done == (uint32_t)nb - 1) {
-            __hip_atomic_store(&ctl[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(&ctl[0], e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        ar_signal_peers(peers, rank, world, b, 2 * e - 1);
+        s_ok = ar_wait_peers(peers, rank, world, b, 2 * e - 1, ctl, spin_limit);
+    }
+    __syncthreads();
+    if (s_ok) {
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);
+        // ---- (B) reduce my slice's sub-chunk over the W buffers (my own is peers.data[rank]); write it to out and
+        // back over my buffer for the peers' gather
+        for (int64_t v = rank * sv + c0 + threadIdx.x; v < rank * sv + c1; v += kArThreads) {
+            float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            for (int p = 0; p < world; ++p) {
+                const u16x8 x = reinterpret_cast<const u16x8*>(peers.data[p] + half)[v];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) acc[j] += bf2f(x[j]);
+            }
+            u16x8 o;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[j]);
+            mine[v] = o;
+            dst[v] = o;
         }
     }
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_ok) {
+        ar_signal_peers(peers, rank, world, b, 2 * e);
+        s_ok = ar_wait_peers(peers, rank, world, b, 2 * e, ctl, spin_limit);
+    }
+    __syncthreads();
+    if (s_ok) {
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);
+        // ---- (C) gather every other slice's reduced sub-chunk from its owner
+        for (int p = 0; p < world; ++p) {
+            if (p == rank) continue;
+            const u16x8* theirs = reinterpret_cast<const u16x8*>(peers.data[p] + half);
+            for (int64_t v = p * sv + c0 + threadIdx.x; v < p * sv + c1; v += kArThreads) dst[v] = theirs[v];
+        }
+    }
+    ar_finish_call(ctl, e, nb);
 }
 
 // ------------------------------------------------------------------------------------------------------------------
@@ -174,14 +266,22 @@ struct IpcAllReduce {
         }
     }
 
-    void run(const uint16_t* in, uint16_t* out, int64_t n, int64_t spin_limit, hipStream_t st) {
+    // algo: 1 = one-shot, 2 = two-shot (needs n % (8 * world) == 0)
+    void run(const uint16_t* in, uint16_t* out, int64_t n, int64_t spin_limit, int algo, hipStream_t st) {
         if (n == 0) return;
         if (n % 8 || n > half_elems) throw std::runtime_error("allreduce: n must be a multiple of 8 and fit the buffer");
-        int64_t nb = (n / 8 + kArThreads * 2 - 1) / (kArThreads * 2);  // >= 2 vectors per thread
+        if (algo == 2 && n % (8 * world)) throw std::runtime_error("allreduce: two-shot needs n % (8 * world) == 0");
+        // >= 2 vectors per thread: of the whole message (one-shot), of one slice (two-shot)
+        const int64_t vec = algo == 2 ? n / 8 / world : n / 8;
+        int64_t nb = (vec + kArThreads * 2 - 1) / (kArThreads * 2);
         if (nb > kArMaxBlocks) nb = kArMaxBlocks;
         if (nb < 1) nb = 1;
-        hipLaunchKernelGGL(allreduce_kernel, dim3((unsigned)nb), dim3(kArThreads), 0, st, peers, in, out, n,
-                           half_elems, rank, world, ctl, spin_limit);
+        if (algo == 2)
+            hipLaunchKernelGGL(allreduce2_kernel, dim3((unsigned)nb), dim3(kArThreads), 0, st, peers, in, out, n,
+                               half_elems, rank, world, ctl, spin_limit);
+        else
+            hipLaunchKernelGGL(allreduce_kernel, dim3((unsigned)nb), dim3(kArThreads), 0, st, peers, in, out, n,
+                               half_elems, rank, world, ctl, spin_limit);
     }
 
     uint32_t error() const {
@@ -202,8 +302,8 @@ struct IpcAllReduce {
 void* ar_create(int rank, int world, int64_t max_bytes) { return new IpcAllReduce(rank, world, max_bytes); }
 std::vector<uint8_t> ar_handles(void* h) { return static_cast<IpcAllReduce*>(h)->handles(); }
 void ar_open(void* h, const std::vector<std::vector<uint8_t>>& all) { static_cast<IpcAllReduce*>(h)->open(all); }
-void ar_run(void* h, const uint16_t* in, uint16_t* out, int64_t n, int64_t spin_limit, hipStream_t st) {
-    static_cast<IpcAllReduce*>(h)->run(in, out, n, spin_limit, st);
+void ar_run(void* h, const uint16_t* in, uint16_t* out, int64_t n, int64_t spin_limit, int algo, hipStream_t st) {
+    static_cast<IpcAllReduce*>(h)->run(in, out, n, spin_limit, algo, st);
 }
 uint32_t ar_error(void* h) { return static_cast<IpcAllReduce*>(h)->error(); }
 int64_t ar_capacity(void* h) { return static_cast<IpcAllReduce*>(h)->half_elems; }

@@ -40,7 +40,7 @@ void launch_gemm(const uint16_t*, const uint16_t*, uint16_t*, int, int, int, boo
 void* ar_create(int, int, int64_t);
 std::vector<uint8_t> ar_handles(void*);
 void ar_open(void*, const std::vector<std::vector<uint8_t>>&);
-void ar_run(void*, const uint16_t*, uint16_t*, int64_t, int64_t, hipStream_t);
+void ar_run(void*, const uint16_t*, uint16_t*, int64_t, int64_t, int, hipStream_t);
 uint32_t ar_error(void*);
 int64_t ar_capacity(void*);
 void ar_destroy(void*);
@@ -515,14 +515,15 @@ void ar_open(int64_t h, const Tensor& all) {
     }
     chronos::ar_open(reinterpret_cast<void*>(h), v);
 }
-void ar_all_reduce(int64_t h, const Tensor& inp, const Tensor& out, int64_t spin_limit) {
+void ar_all_reduce(int64_t h, const Tensor& inp, const Tensor& out, int64_t spin_limit, int64_t algo) {
     chk_bf16(inp, "inp");
     chk_bf16(out, "out");
     CHK(inp.numel() == out.numel(), "ar_all_reduce: size mismatch");
     CHK(inp.numel() % 8 == 0 && inp.numel() <= chronos::ar_capacity(reinterpret_cast<void*>(h)),
         "ar_all_reduce: numel must be % 8 and fit the IPC buffer");
     c10::hip::HIPGuardMasqueradingAsCUDA g(inp.device());
-    chronos::ar_run(reinterpret_cast<void*>(h), bf(inp), bfm(out), inp.numel(), spin_limit, cur_stream());
+    CHK(algo == 1 || algo == 2, "ar_all_reduce: algo must be 1 (one-shot) or 2 (two-shot)");
+    chronos::ar_run(reinterpret_cast<void*>(h), bf(inp), bfm(out), inp.numel(), spin_limit, (int)algo, cur_stream());
 }
 int64_t ar_error(int64_t h) { return chronos::ar_error(reinterpret_cast<void*>(h)); }
 int64_t ar_capacity(int64_t h) { return chronos::ar_capacity(reinterpret_cast<void*>(h)); }
@@ -553,7 +554,7 @@ TORCH_LIBRARY(chronos, m) {
     m.def("ar_create(int rank, int world, int max_bytes) -> int", &ar_create);
     m.def("ar_handles(int h) -> Tensor", &ar_handles);
     m.def("ar_open(int h, Tensor all) -> ()", &ar_open);
-    m.def("ar_all_reduce(int h, Tensor inp, Tensor(a!) out, int spin_limit) -> ()");
+    m.def("ar_all_reduce(int h, Tensor inp, Tensor(a!) out, int spin_limit, int algo=1) -> ()");
     m.def("ar_error(int h) -> int", &ar_error);
     m.def("ar_capacity(int h) -> int", &ar_capacity);
     m.def("ar_destroy(int h) -> ()", &ar_destroy);

@@ -1,4 +1,5 @@
-"""IPC one-shot all-reduce for tensor-parallel decode (kernel: csrc/kernels/allreduce.hip).
+"""IPC one-shot / two-shot all-reduce for tensor-parallel decode (kernel:
+csrc/kernels/allreduce.hip).
 
 Every TP rank owns a bf16 exchange buffer (two parity halves) plus an uncached flag array; the IPC handles are
 swapped once over the (gloo or RCCL) process group and every rank maps all peers' buffers.  ``all_reduce(x)`` is one
@@ -6,6 +7,12 @@ kernel launch: publish my shard, flag every peer, wait for every peer's flag, re
 one hop instead of a ring's 2(W-1), which is what decode-sized messages (16 KiB x tokens) are bound by.  The launch
 takes no host-side state (the epoch lives on the device), so it is captured inside the decode hipGraph like any
 other kernel.  Larger messages (prefill chunks) stay on RCCL (``TPContext.all_reduce`` picks by size).
+
+Mid-sized messages (70B TP8 decode at large batch: 1-8 MiB) take the two-shot form: reduce-scatter of W slices
+through the same exchange buffers, then an all-gather of the reduced slices.  Each rank moves 2(W-1)/W of the
+message over xGMI instead of one-shot's W-1 copies, at the price of a second dependent hop.  Per link that is N
+bytes (one-shot) against 2N/W (two-shot): at W = 8 two-shot wins once the saved 3N/4 outweighs one extra
+flag hop (~5 us, i.e. around half a MiB at ~60 GB/s per link); at W <= 2 it saves nothing and is never picked.
 
 A peer that never arrives makes the kernel give up after a bounded spin and set an error word (checked by
 :meth:`check`), rather than hanging the GPU.
@@ -18,7 +25,7 @@ import torch.distributed as dist
 
 class IpcAllReduce:
     def __init__(self, group=None, max_bytes: int = 8 << 20, device: torch.device | None = None,
-                 spin_limit: int = 20_000_000):
+                 spin_limit: int = 20_000_000, two_shot_min_bytes: int = 512 << 10):
         from .. import ops
 
         ops.load()
@@ -29,6 +36,7 @@ class IpcAllReduce:
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.max_bytes = max_bytes
         self.spin_limit = spin_limit
+        self.two_shot_min_bytes = two_shot_min_bytes
         with torch.cuda.device(self.device):
             self.h = self.C.ar_create(self.rank, self.world, max_bytes)
         mine = self.C.ar_handles(self.h)
@@ -42,11 +50,19 @@ class IpcAllReduce:
     def fits(self, x: torch.Tensor) -> bool:
         return x.dtype == torch.bfloat16 and x.is_cuda and x.numel() % 8 == 0 and x.numel() <= self.capacity
 
-    def all_reduce(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
-        """Sum of ``x`` over the group (a new tensor unless ``out`` is given; may alias ``x``)."""
+    def pick(self, x: torch.Tensor) -> int:
+        """1 = one-shot, 2 = two-shot (needs numel % (8 * world) == 0)."""
+        if self.world > 2 and x.numel() * x.element_size() >= self.two_shot_min_bytes \
+                and x.numel() % (8 * self.world) == 0:
+            return 2
+        return 1
+
+    def all_reduce(self, x: torch.Tensor, out: torch.Tensor | None = None, algo: int = 0) -> torch.Tensor:
+        """Sum of ``x`` over the group (a new tensor unless ``out`` is given; may alias ``x``).  ``algo`` 0 picks by
+        size (:meth:`pick`); 1 / 2 force one-shot / two-shot.  Every rank must pass the same algo for a call."""
         x = x.contiguous()
         out = torch.empty_like(x) if out is None else out
-        self.C.ar_all_reduce(self.h, x, out, self.spin_limit)
+        self.C.ar_all_reduce(self.h, x, out, self.spin_limit, algo or self.pick(x))
         return out
 
     def check(self) -> None:

@@ -49,8 +49,9 @@ class TPContext:
         return x, dist.all_reduce(x, group=self.group, async_op=True)
 
     def enable_ipc_allreduce(self, max_bytes: int = 8 << 20, threshold: int = 4 << 20):
-        """Route bf16 all-reduces of at most ``threshold`` bytes to the IPC one-shot kernel (K14); larger messages
-        (prefill chunks), where a ring's link bandwidth wins over one-shot's W-fold reads, stay on RCCL."""
+        """Route bf16 all-reduces of at most ``threshold`` bytes to the IPC kernels (K14: one-shot for small messages,
+        two-shot above ``IpcAllReduce.two_shot_min_bytes`` at W > 2); larger messages (prefill chunks), where RCCL's
+        multi-channel rings use the links best, stay on RCCL."""
         from .custom_ar import IpcAllReduce
 
         ar = IpcAllReduce(self.group, max_bytes)

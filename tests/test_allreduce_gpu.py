@@ -1,9 +1,10 @@
-"""IPC one-shot all-reduce (csrc/kernels/allreduce.hip, K14) with two ranks sharing the box's one GPU.
+"""IPC one-shot / two-shot all-reduce (csrc/kernels/allreduce.hip, K14) with 2 or 4 ranks sharing the box's one GPU.
 
 Both processes map each other's exchange buffers through hipIpc handles swapped over gloo, exactly as TP ranks on
 different GPUs do over xGMI.  Checks: bit-exact sums (fp32 accumulation in rank order, one bf16 rounding) over many
-calls of different sizes (parity halves + device epochs), in-place use, hipGraph capture + replay, and that the
-bounded spin reports (not hangs) when a peer never arrives."""
+calls of different sizes (parity halves + device epochs), both algorithms interleaved call by call (one flag array,
+monotonic values), in-place use, hipGraph capture + replay, and that the bounded spin reports (not hangs) when a peer
+never arrives."""
 import os
 import socket
 
@@ -45,17 +46,19 @@ def _worker(rank, world, port, q):
     try:
         ar = IpcAllReduce(max_bytes=4 << 20, spin_limit=50_000_000)
         step = 0
-        for n in (8, 4096, 8 * 1000, 1 << 20, 8, 65536):
-            for _ in range(3):
+        for n in (8, 4096, 8 * 1000, 1 << 20, 8, 65536, 96 * world):
+            for algo in (1, 2, 0):
+                if algo == 2 and n % (8 * world):
+                    algo = 1
                 x = _inputs(rank, step, n).cuda()
                 dist.barrier()
-                y = ar.all_reduce(x, out=x if step % 2 else None)  # alternate in-place / out-of-place
+                y = ar.all_reduce(x, out=x if step % 2 else None, algo=algo)  # alternate in-place / out-of-place
                 torch.cuda.synchronize()
                 if not torch.equal(y.cpu(), _expected(world, step, n)):
-                    res = {"ok": False, "msg": f"mismatch n={n} step={step}"}
+                    res = {"ok": False, "msg": f"mismatch n={n} algo={algo} step={step}"}
                 step += 1
         ar.check()
-        # graph capture: 3 all-reduces of fixed buffers, replayed with new data
+        # graph capture: 3 all-reduces of fixed buffers (one-shot, two-shot, one-shot), replayed with new data
         n = 12288
         bufs = [torch.empty(n, dtype=torch.bfloat16, device="cuda") for _ in range(3)]
         outs = [torch.empty_like(b) for b in bufs]
@@ -64,8 +67,8 @@ def _worker(rank, world, port, q):
         s = torch.cuda.Stream()
         with torch.cuda.stream(s):
             with torch.cuda.graph(g):
-                for b, o in zip(bufs, outs):
-                    ar.all_reduce(b, out=o)
+                for i, (b, o) in enumerate(zip(bufs, outs)):
+                    ar.all_reduce(b, out=o, algo=2 if i == 1 else 1)
         torch.cuda.synchronize()
         for rep in range(4):
             for i, b in enumerate(bufs):
@@ -99,16 +102,17 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_ipc_allreduce_two_ranks_one_gpu():
+@pytest.mark.parametrize("world", [2, 4])
+def test_ipc_allreduce_ranks_share_one_gpu(world):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in ps:
         p.start()
-    got = dict(q.get(timeout=300) for _ in range(2))
+    got = dict(q.get(timeout=100) for _ in range(world))
     for p in ps:
         p.join(timeout=60)
-    assert got[0]["ok"] and got[1]["ok"], got
+    assert all(got[r]["ok"] for r in range(world)), got
