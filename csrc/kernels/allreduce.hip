@@ -203,6 +203,86 @@ __global__ void __launch_bounds__(kArThreads) allreduce2_kernel(ArPeers peers, c
     ar_finish_call(ctl, e, nb);
 }
 
+// One-shot all-reduce fused with the residual add and RMSNorm that follow every row-parallel projection in a TP
+// layer: resid <- bf16(bf16(sum of the W partials) + resid), y <- rmsnorm(resid) * w.  Same
+// exchange protocol and flag values as allreduce_kernel (the two interleave freely), but each block owns whole rows,
+// so the norm's sum of squares is a block reduction and the normalised rows leave in the same launch: one launch and
+// one [T, d] round trip fewer per projection.  Rounding is the unfused path's exactly (all-reduce output in bf16,
+// then rmsnorm_kernel<RESID=true>'s arithmetic).
+template <int MAXV>
+__global__ void __launch_bounds__(kArThreads) allreduce_norm_kernel(
+    ArPeers peers, const uint16_t* __restrict__ in, uint16_t* __restrict__ resid, const uint16_t* __restrict__ w,
+    uint16_t* __restrict__ y, int64_t rows, int d, float eps, int64_t half_elems, int rank, int world,
+    uint32_t* __restrict__ ctl, int64_t spin_limit) {
+    __shared__ uint32_t s_epoch;
+    __shared__ int s_ok;
+    __shared__ float red[16];
+    const int b = blockIdx.x, nb = gridDim.x;
+    if (threadIdx.x == 0) s_epoch = __hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1;
+    __syncthreads();
+    const uint32_t e = s_epoch;
+    const int nv = d / 8;
+    const int64_t rpb = (rows + nb - 1) / nb;
+    const int64_t r0 = (int64_t)b * rpb, r1 = r0 + rpb < rows ? r0 + rpb : rows;
+    const int64_t half = (int64_t)(e & 1) * half_elems;
+    u16x8* mine = reinterpret_cast<u16x8*>(peers.data[rank] + half);
+
+    // ---- publish this block's rows
+    for (int64_t v = r0 * nv + threadIdx.x; v < r1 * nv; v += kArThreads)
+        mine[v] = reinterpret_cast<const u16x8*>(in)[v];
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        ar_signal_peers(peers, rank, world, b, 2 * e - 1);
+        s_ok = ar_wait_peers(peers, rank, world, b, 2 * e - 1, ctl, spin_limit);
+    }
+    __syncthreads();
+    if (s_ok) {
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);
+        const u16x8* wv = reinterpret_cast<const u16x8*>(w);
+        for (int64_t r = r0; r < r1; ++r) {
+            u16x8* rv = reinterpret_cast<u16x8*>(resid + r * d);
+            u16x8* yv = reinterpret_cast<u16x8*>(y + r * d);
+            float vals[MAXV][8];
+            float ss = 0.f;
+#pragma unroll
+            for (int k = 0; k < MAXV; ++k) {
+                const int i = threadIdx.x + k * kArThreads;
+                if (i < nv) {
+                    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                    for (int p = 0; p < world; ++p) {
+                        const u16x8 x = reinterpret_cast<const u16x8*>(peers.data[p] + half)[r * nv + i];
+#pragma unroll
+                        for (int j = 0; j < 8; ++j) acc[j] += bf2f(x[j]);
+                    }
+                    const u16x8 old = rv[i];
+                    u16x8 nr;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        nr[j] = f2bf(bf2f(f2bf(acc[j])) + bf2f(old[j]));
+                        vals[k][j] = bf2f(nr[j]);
+                        ss += vals[k][j] * vals[k][j];
+                    }
+                    rv[i] = nr;
+                }
+            }
+            const float inv = rsqrtf(block_sum(ss, red) / (float)d + eps);
+#pragma unroll
+            for (int k = 0; k < MAXV; ++k) {
+                const int i = threadIdx.x + k * kArThreads;
+                if (i < nv) {
+                    const u16x8 g = wv[i];
+                    u16x8 o;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(f2bf(vals[k][j] * inv)) * bf2f(g[j]));
+                    yv[i] = o;
+                }
+            }
+        }
+    }
+    ar_finish_call(ctl, e, nb);
+}
+
 // ------------------------------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------------------------------
@@ -284,6 +364,25 @@ struct IpcAllReduce {
                                half_elems, rank, world, ctl, spin_limit);
     }
 
+    // rows x d bf16 partials -> resid (in place) and y; d % 8 == 0, d <= 8 * kArThreads * 8
+    void run_norm(const uint16_t* in, uint16_t* resid, const uint16_t* w, uint16_t* y, int64_t rows, int d, float eps,
+                  int64_t spin_limit, hipStream_t st) {
+        if (rows == 0) return;
+        if (d % 8 || rows * d > half_elems) throw std::runtime_error("allreduce_norm: d % 8 and rows * d <= capacity");
+        const int vpt = (d / 8 + kArThreads - 1) / kArThreads;
+        int64_t nb = rows < kArMaxBlocks ? rows : kArMaxBlocks;
+        const dim3 g((unsigned)nb), blk(kArThreads);
+#define ARN_CASE(V)                                                                                              \
+    if (vpt <= V) {                                                                                              \
+        hipLaunchKernelGGL((allreduce_norm_kernel<V>), g, blk, 0, st, peers, in, resid, w, y, rows, d, eps,       \
+                           half_elems, rank, world, ctl, spin_limit);                                            \
+        return;                                                                                                  \
+    }
+        ARN_CASE(1) ARN_CASE(2) ARN_CASE(4) ARN_CASE(8)
+#undef ARN_CASE
+        throw std::runtime_error("allreduce_norm: d too large");
+    }
+
     uint32_t error() const {
         uint32_t v = 0;
         hip_ok(hipMemcpy(&v, ctl + 2, sizeof(v), hipMemcpyDeviceToHost), "read error word");
@@ -304,6 +403,10 @@ std::vector<uint8_t> ar_handles(void* h) { return static_cast<IpcAllReduce*>(h)-
 void ar_open(void* h, const std::vector<std::vector<uint8_t>>& all) { static_cast<IpcAllReduce*>(h)->open(all); }
 void ar_run(void* h, const uint16_t* in, uint16_t* out, int64_t n, int64_t spin_limit, int algo, hipStream_t st) {
     static_cast<IpcAllReduce*>(h)->run(in, out, n, spin_limit, algo, st);
+}
+void ar_run_norm(void* h, const uint16_t* in, uint16_t* resid, const uint16_t* w, uint16_t* y, int64_t rows, int d,
+                 float eps, int64_t spin_limit, hipStream_t st) {
+    static_cast<IpcAllReduce*>(h)->run_norm(in, resid, w, y, rows, d, eps, spin_limit, st);
 }
 uint32_t ar_error(void* h) { return static_cast<IpcAllReduce*>(h)->error(); }
 int64_t ar_capacity(void* h) { return static_cast<IpcAllReduce*>(h)->half_elems; }

@@ -41,6 +41,8 @@ void* ar_create(int, int, int64_t);
 std::vector<uint8_t> ar_handles(void*);
 void ar_open(void*, const std::vector<std::vector<uint8_t>>&);
 void ar_run(void*, const uint16_t*, uint16_t*, int64_t, int64_t, int, hipStream_t);
+void ar_run_norm(void*, const uint16_t*, uint16_t*, const uint16_t*, uint16_t*, int64_t, int, float, int64_t,
+                 hipStream_t);
 uint32_t ar_error(void*);
 int64_t ar_capacity(void*);
 void ar_destroy(void*);
@@ -525,6 +527,20 @@ void ar_all_reduce(int64_t h, const Tensor& inp, const Tensor& out, int64_t spin
     CHK(algo == 1 || algo == 2, "ar_all_reduce: algo must be 1 (one-shot) or 2 (two-shot)");
     chronos::ar_run(reinterpret_cast<void*>(h), bf(inp), bfm(out), inp.numel(), spin_limit, (int)algo, cur_stream());
 }
+// fused one-shot all-reduce + residual add + RMSNorm: resid <- bf16(sum(inp) + resid), y <- rmsnorm(resid) * w
+void ar_all_reduce_norm(int64_t h, const Tensor& inp, const Tensor& resid, const Tensor& w, const Tensor& y, double eps,
+                        int64_t spin_limit) {
+    chk_bf16(inp, "inp");
+    chk_bf16(resid, "resid");
+    chk_bf16(w, "w");
+    chk_bf16(y, "y");
+    CHK(inp.dim() == 2 && resid.sizes() == inp.sizes() && y.sizes() == inp.sizes(), "ar_all_reduce_norm: [T, d] rows");
+    CHK(w.numel() == inp.size(1) && inp.size(1) % 8 == 0 && inp.size(1) <= 8 * 256 * 8, "ar_all_reduce_norm: d");
+    CHK(inp.numel() <= chronos::ar_capacity(reinterpret_cast<void*>(h)), "ar_all_reduce_norm: exceeds the IPC buffer");
+    c10::hip::HIPGuardMasqueradingAsCUDA g(inp.device());
+    chronos::ar_run_norm(reinterpret_cast<void*>(h), bf(inp), bfm(resid), bf(w), bfm(y), inp.size(0),
+                         (int)inp.size(1), (float)eps, spin_limit, cur_stream());
+}
 int64_t ar_error(int64_t h) { return chronos::ar_error(reinterpret_cast<void*>(h)); }
 int64_t ar_capacity(int64_t h) { return chronos::ar_capacity(reinterpret_cast<void*>(h)); }
 void ar_destroy(int64_t h) { chronos::ar_destroy(reinterpret_cast<void*>(h)); }
@@ -555,6 +571,7 @@ TORCH_LIBRARY(chronos, m) {
     m.def("ar_handles(int h) -> Tensor", &ar_handles);
     m.def("ar_open(int h, Tensor all) -> ()", &ar_open);
     m.def("ar_all_reduce(int h, Tensor inp, Tensor(a!) out, int spin_limit, int algo=1) -> ()");
+    m.def("ar_all_reduce_norm(int h, Tensor inp, Tensor(a!) resid, Tensor w, Tensor(b!) y, float eps, int spin_limit) -> ()");
     m.def("ar_error(int h) -> int", &ar_error);
     m.def("ar_capacity(int h) -> int", &ar_capacity);
     m.def("ar_destroy(int h) -> ()", &ar_destroy);
@@ -583,4 +600,5 @@ TORCH_LIBRARY_IMPL(chronos, CUDA, m) {
     m.impl("paged_attention", &paged_attention);
     m.impl("constrained_sample", &constrained_sample);
     m.impl("ar_all_reduce", &ar_all_reduce);
+    m.impl("ar_all_reduce_norm", &ar_all_reduce_norm);
 }

@@ -28,6 +28,7 @@ from ..parallel.tp import TPContext
 # decode steps (T <= 2, TP=1): residual add + norm partials in the producing GEMV's epilogue, the norm in the consuming
 # GEMV's prologue, RoPE + paged-KV write in the QKV GEMV's epilogue (CHRONOS_FUSE_NORM=0: the separate kernels)
 _FUSE_NORM = os.environ.get("CHRONOS_FUSE_NORM", "1") != "0"
+_FUSE_AR_NORM = os.environ.get("CHRONOS_FUSE_AR_NORM", "1") != "0"  # TP: fused IPC all-reduce + residual + RMSNorm
 
 
 @dataclass
@@ -551,11 +552,14 @@ class LlamaModel:
         self.sequence_parallel = False
 
     # ---- one micro-batch's pieces of a layer (bf16: x is a tensor; W8A8: x is (e4m3 bytes, row scales)) ----------
-    def _norm(self, h, st: dict, w: torch.Tensor, first: bool = False):
+    def _norm(self, h, st: dict, w: torch.Tensor, first: bool = False, reduce: bool = False):
         """(st["resid"] <- h + st["resid"]) and the normalised projection input (first: the residual stream starts as
         h itself).  When h is an ops.ResidOut (a decode producer already added the residual and summed the squares)
-        the result is an ops.LazyNorm that the consuming GEMV folds into its prologue: no norm launch."""
+        the result is an ops.LazyNorm that the consuming GEMV folds into its prologue: no norm launch.  ``reduce``: h
+        is still this rank's partial sum; the TP all-reduce, residual add and norm run as one fused IPC launch."""
         eps = self.cfg.rms_eps
+        if reduce:
+            return self.tp.all_reduce_add_rmsnorm(h, st["resid"], w, eps)
         if isinstance(h, ops.ResidOut):
             st["resid"] = h.s
             return ops.LazyNorm(h.s, h.part, w, eps)
@@ -644,7 +648,15 @@ class LlamaModel:
             return self._forward_sp(sb, kv, logits_dtype)
         parts = sb.parts if (sb.parts and tp.world > 1) else [sb]
         overlap = len(parts) > 1
-        ar = (lambda t: tp.all_reduce_async(t)) if overlap else (lambda t: (tp.all_reduce(t), None))  # noqa: E731
+        # TP, one part: the all-reduce after o_proj / down_proj is fused with the residual add + RMSNorm that follows
+        # (IPC kernel; tp.all_reduce_add_rmsnorm falls back to the two steps for messages it cannot take)
+        fuse = (not overlap and tp.world > 1 and tp.fast_allreduce_norm is not None and not w.fp8 and _FUSE_AR_NORM)
+        if overlap:
+            ar = lambda t: tp.all_reduce_async(t)  # noqa: E731
+        elif fuse:
+            ar = lambda t: (t, None)  # noqa: E731 — reduced inside _norm
+        else:
+            ar = lambda t: (tp.all_reduce(t), None)  # noqa: E731
         states = []
         for p in parts:
             h = tp.all_reduce(ops.embedding(p.ids, w.embed, w.vocab_start))
@@ -659,16 +671,20 @@ class LlamaModel:
             for st, (o, work) in zip(states, pend):
                 if work is not None:
                     work.wait()
-                st["x"] = self._norm(o, st, lw.mlp_norm)
+                st["x"] = self._norm(o, st, lw.mlp_norm, reduce=fuse)
                 pend2.append(ar(self._mlp(lw, st)))
             for st, (dn, work) in zip(states, pend2):
                 if work is not None:
                     work.wait()
                 if li + 1 < L:
-                    st["x"] = self._norm(dn, st, w.layers[li + 1].attn_norm)
+                    st["x"] = self._norm(dn, st, w.layers[li + 1].attn_norm, reduce=fuse)
                 elif isinstance(dn, ops.ResidOut) and st["sb"].tiles is None:  # decode: every token is sampled
                     st["x"] = self._norm(dn, st, w.norm)
+                elif fuse and st["sb"].tiles is None:  # TP decode: every token is sampled
+                    st["x"] = self._norm(dn, st, w.norm, reduce=True)
                 else:  # only the sampled rows need the final norm + LM head (bf16)
+                    if fuse:
+                        dn = tp.all_reduce(dn)
                     li_ = st["sb"].last_idx
                     st["x"] = ops.add_rmsnorm(dn.index_select(0, li_), st["resid"].index_select(0, li_), w.norm,
                                               cfg.rms_eps)

@@ -65,6 +65,16 @@ class IpcAllReduce:
         self.C.ar_all_reduce(self.h, x, out, self.spin_limit, algo or self.pick(x))
         return out
 
+    def all_reduce_norm(self, x: torch.Tensor, resid: torch.Tensor, w: torch.Tensor, eps: float,
+                        out: torch.Tensor | None = None) -> torch.Tensor:
+        """One-shot all-reduce of the [T, d] partials fused with the residual add and RMSNorm that follow a
+        row-parallel projection: ``resid <- bf16(sum(x) + resid)`` in place, returns ``rmsnorm(resid) * w`` (the
+        unfused all_reduce + ops.add_rmsnorm bit for bit, one launch)."""
+        x = x.contiguous()
+        out = torch.empty_like(x) if out is None else out
+        self.C.ar_all_reduce_norm(self.h, x, resid, w, out, eps, self.spin_limit)
+        return out
+
     def check(self) -> None:
         if self.C.ar_error(self.h):
             raise RuntimeError("IPC all-reduce: a peer did not arrive within the spin limit (rank desync?)")

@@ -22,6 +22,8 @@ class TPContext:
     world: int = 1
     group: Optional[object] = None
     fast_allreduce: Optional[Callable[[torch.Tensor], Optional[torch.Tensor]]] = None
+    # (x, resid, w, eps) -> normalised rows, or None when the fused IPC kernel cannot take the message
+    fast_allreduce_norm: Optional[Callable[..., Optional[torch.Tensor]]] = None
 
     @classmethod
     def single(cls) -> "TPContext":
@@ -61,9 +63,27 @@ class TPContext:
                 return ar.all_reduce(x, out=x)
             return None
 
+        def fast_norm(x: torch.Tensor, resid: torch.Tensor, w: torch.Tensor, eps: float) -> Optional[torch.Tensor]:
+            if (x.numel() * x.element_size() <= threshold and ar.fits(x) and x.dim() == 2 and x.is_contiguous()
+                    and resid.is_contiguous() and x.shape[1] % 8 == 0 and x.shape[1] <= 16384):
+                return ar.all_reduce_norm(x, resid, w, eps)
+            return None
+
         self.fast_allreduce = fast
+        self.fast_allreduce_norm = fast_norm
         self.ipc_allreduce = ar
         return ar
+
+    def all_reduce_add_rmsnorm(self, x: torch.Tensor, resid: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+        """resid <- bf16(sum over ranks of x + resid) in place; returns rmsnorm(resid) * w.  One launch on the fused
+        IPC kernel (K14 + residual + RMSNorm) when it takes the message, else all-reduce then ops.add_rmsnorm."""
+        if self.fast_allreduce_norm is not None:
+            y = self.fast_allreduce_norm(x, resid, w, eps)
+            if y is not None:
+                return y
+        from .. import ops
+
+        return ops.add_rmsnorm(self.all_reduce(x), resid, w, eps)
 
     def reduce_scatter_rows(self, x: torch.Tensor) -> torch.Tensor:
         """Sequence parallelism: sum over ranks of x [R * world, ...], this rank keeping rows [rank * R, (rank + 1) * R)

@@ -25,6 +25,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("path", help="a kernel_trace.csv or a directory searched for one")
     ap.add_argument("--min-us", type=float, default=20.0)
+    ap.add_argument("--max-us", type=float, default=0.0,
+                    help="only gaps below this go into the pair table (e.g. 50: inter-kernel gaps inside a graph)")
     ap.add_argument("--top", type=int, default=25)
     ap.add_argument("--last-ms", type=float, default=0.0, help="analyse only the final window of this length")
     a = ap.parse_args()
@@ -56,7 +58,7 @@ def main():
                 if g < b:
                     hist[b] += 1
                     break
-            if g >= a.min_us:
+            if g >= a.min_us and (a.max_us <= 0 or g < a.max_us):
                 k = (short(prev), short(n))
                 gaps[k][0] += 1
                 gaps[k][1] += g
@@ -68,7 +70,7 @@ def main():
           + ", ".join(f"<{int(b) if b < 1e12 else 'inf'}: {c}" for b, c in sorted(hist.items())))
     print(f"gaps >= {a.min_us} us by (previous kernel -> next kernel), largest total first:")
     for (p, n), (c, t) in sorted(gaps.items(), key=lambda kv: -kv[1][1])[:a.top]:
-        print(f"  {t / 1e3:8.2f} ms  {c:6d} x  {p}  ->  {n}")
+        print(f"  {t / 1e3:8.2f} ms  {c:6d} x  {t / c:6.2f} us  {p}  ->  {n}")
 
 
 if __name__ == "__main__":

@@ -81,6 +81,25 @@ def _worker(rank, world, port, q):
                 if not torch.equal(o.cpu(), _expected(world, 500 + 3 * rep + i, n)):
                     res = {"ok": False, "msg": f"graph mismatch rep={rep} i={i}"}
         ar.check()
+        # fused all-reduce + residual add + RMSNorm == all-reduce then ops.add_rmsnorm, bit for bit
+        from chronos import ops
+
+        for T, d in ((1, 4096), (5, 8192), (70, 1024), (3, 16384), (130, 256)):
+            x = _inputs(rank, step, T * d).view(T, d).cuda()
+            g = torch.Generator().manual_seed(77 + T)
+            resid = torch.randn(T, d, generator=g).to(torch.bfloat16).cuda()
+            w = (1 + 0.1 * torch.randn(d, generator=g)).to(torch.bfloat16).cuda()
+            r_ref = resid.clone()
+            y_ref = ops.add_rmsnorm(_expected(world, step, T * d).view(T, d).cuda(), r_ref, w, 1e-5)
+            dist.barrier()
+            y = ar.all_reduce_norm(x, resid, w, 1e-5)
+            ar.all_reduce(x.view(-1).clone(), algo=1)  # interleave a plain call: shared epochs / flags
+            torch.cuda.synchronize()
+            if not (torch.equal(y, y_ref) and torch.equal(resid, r_ref)):
+                res = {"ok": False, "msg": f"fused norm mismatch T={T} d={d}: "
+                                           f"{(y.float() - y_ref.float()).abs().max().item()}"}
+            step += 1
+        ar.check()
         # a missing peer: only rank 0 calls; its kernel must give up and flag the error
         dist.barrier()
         if rank == 0:
@@ -116,3 +135,74 @@ def test_ipc_allreduce_ranks_share_one_gpu(world):
     for p in ps:
         p.join(timeout=60)
     assert all(got[r]["ok"] for r in range(world)), got
+
+
+def _engine_worker(rank, world, port, q):
+    """TP engine on the shared GPU: decode with the fused all-reduce + norm must produce the same tokens as the
+    unfused path (the fused kernel is bit-exact), and must actually run."""
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    from chronos.brain.engine.engine import Engine, EngineConfig
+    from chronos.models import llama
+    from chronos.parallel.tp import TPContext
+    from chronos.sensor.prompt import VERDICT_SCHEMA, build_prompt
+
+    res = {"ok": True, "msg": ""}
+    try:
+        tp = TPContext.from_group()
+        tp.enable_ipc_allreduce()
+        fused_calls = [0]
+        inner = tp.fast_allreduce_norm
+
+        def counting(*a):
+            y = inner(*a)
+            fused_calls[0] += y is not None
+            return y
+
+        tp.fast_allreduce_norm = counting
+
+        def gather_last(x):  # gloo has no CUDA all_gather: go through the host
+            parts = [torch.empty_like(x.cpu()) for _ in range(world)]
+            dist.all_gather(parts, x.contiguous().cpu())
+            return torch.cat(parts, dim=-1).to(x.device)
+
+        tp.all_gather_last = gather_last
+        chains = [["[OPEN] attack_chain.sh -> /tmp/malware.bin", "[EXEC] attack_chain.sh -> curl"],
+                  ["[EXEC] bash -> chmod", "[OPEN] chmod -> "]]
+        outs = {}
+        for fuse in (True, False):
+            llama._FUSE_AR_NORM = fuse
+            cfg = EngineConfig(model="tiny", device="cuda", max_slots=4, max_model_len=384, use_graphs=False,
+                               decode_burst=4, seed=0)
+            eng = Engine(cfg, tp=tp)
+            reqs = [eng.submit(build_prompt(c), fmt=VERDICT_SCHEMA, num_predict=24) for c in chains]
+            eng.run_until_idle()
+            outs[fuse] = [r.out_ids for r in reqs]
+        tp.ipc_allreduce.check()
+        if outs[True] != outs[False]:
+            res = {"ok": False, "msg": f"fused {outs[True]} != unfused {outs[False]}"}
+        elif fused_calls[0] == 0:
+            res = {"ok": False, "msg": "fused all-reduce + norm never ran"}
+    except Exception as e:  # noqa: BLE001
+        res = {"ok": False, "msg": repr(e)}
+    q.put((rank, res))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_tp2_engine_fused_allreduce_norm_matches_unfused():
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    ps = [ctx.Process(target=_engine_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=110) for _ in range(2))
+    for p in ps:
+        p.join(timeout=60)
+    assert got[0]["ok"] and got[1]["ok"], got
