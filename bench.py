@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--num-predict", type=int, default=64)
     ap.add_argument("--single-stream", type=int, default=16, help="chains for the single-stream p50 latency")
     ap.add_argument("--burst", type=int, default=8)
+    ap.add_argument("--tail-burst", type=int, default=4,
+                    help="decode steps per burst once a >=128-row bucket has started to drain (0 = always --burst)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-prefix-cache", action="store_true")
     ap.add_argument("--async-harvest", action="store_true")
@@ -131,7 +133,8 @@ def main():
         if cuda:
             tp.enable_ipc_allreduce()
     cfg = EngineConfig(model=a.model, device=str(device), max_slots=a.streams, max_model_len=a.max_model_len,
-                       default_num_predict=a.num_predict, decode_burst=a.burst, use_graphs=not a.no_graphs,
+                       default_num_predict=a.num_predict, decode_burst=a.burst, tail_burst=a.tail_burst,
+                       use_graphs=not a.no_graphs,
                        prefix_cache=not a.no_prefix_cache, async_harvest=a.async_harvest, seed=0,
                        prefill_ramp=a.prefill_ramp, jump_forward=not a.no_jump_forward,
                        weight_dtype=a.weights, tp_sequence_parallel=a.sequence_parallel)

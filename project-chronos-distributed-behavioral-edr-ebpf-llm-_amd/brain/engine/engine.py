@@ -63,6 +63,11 @@ class EngineConfig:
     default_num_predict: int = 128
     max_out: int = 512             # hard cap on generated tokens per request
     decode_burst: int = 8
+    # Shorter bursts once a large decode bucket has started to drain (<= tail_burst_fill of its rows live, >= 128
+    # rows): compaction into a smaller bucket happens at harvests, so the tail of a wave sheds finished rows sooner.
+    # 0 disables.
+    tail_burst: int = 4
+    tail_burst_fill: float = 0.9
     use_graphs: bool = True
     grammar_capacity: int = 2048
     max_string: int = 160          # default maxLength for schema strings without one (keeps verdicts short)
@@ -232,7 +237,7 @@ class Engine:
         self.running: dict[int, Request] = {}
         self.free_slots = list(range(S - 1, -1, -1))
         self._rid = itertools.count()
-        self._graphs: dict[tuple[int, int], torch.cuda.CUDAGraph] = {}  # (decode rows, kv splits) -> graph
+        self._graphs: dict[tuple[int, int, int], torch.cuda.CUDAGraph] = {}  # (rows, kv splits, steps) -> graph
         self._graph_pool = None
         self.stats = collections.Counter()
         # host wall seconds per scheduler phase (harvest includes harvest_gpu_wait: the wait for the burst to finish)
@@ -599,14 +604,20 @@ class Engine:
             c *= 2
         return min(c, self.cfg.max_model_len)
 
+    def _burst_len(self, n: int) -> int:
+        k, t = self.cfg.decode_burst, self.cfg.tail_burst
+        if 0 < t < k and n >= 128 and len(self.running) <= self.cfg.tail_burst_fill * n:
+            return t
+        return k
+
     def _decode_burst(self) -> _Snapshot:
         n = min(self._decode_rows(), self.cfg.max_slots)
-        k = self.cfg.decode_burst
+        k = self._burst_len(n)
         ns = self._nsplit(n, self._ctx_class())
         if self.device.type == "cuda" and self.cfg.use_graphs:
-            g = self._graphs.get((n, ns))
+            g = self._graphs.get((n, ns, k))
             if g is None:
-                g = self._capture(n, ns)
+                g = self._capture(n, ns, k)
             g.replay()
         else:
             self._gate(n)
@@ -638,7 +649,7 @@ class Engine:
         if self.device.type == "cuda" and self.cfg.decode_gate:
             ops.set_decode_gate(self.s_state, n if 0 < n <= 8 else 0)
 
-    def _capture(self, n: int, ns: int) -> "torch.cuda.CUDAGraph":
+    def _capture(self, n: int, ns: int, k: int) -> "torch.cuda.CUDAGraph":
         if self._graph_pool is None:
             self._graph_pool = torch.cuda.graph_pool_handle()
         g = torch.cuda.CUDAGraph()
@@ -646,11 +657,11 @@ class Engine:
         self._gate(n)
         try:
             with torch.cuda.graph(g, pool=self._graph_pool):
-                for _ in range(self.cfg.decode_burst):
+                for _ in range(k):
                     self._decode_once(n, ns)
         finally:
             self._gate(0)
-        self._graphs[(n, ns)] = g
+        self._graphs[(n, ns, k)] = g
         self.stats["graphs_captured"] += 1
         return g
 
