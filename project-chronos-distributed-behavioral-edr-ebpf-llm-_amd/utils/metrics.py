@@ -1,8 +1,10 @@
 """Brain observability: Prometheus text metrics + per-request JSONL records.
 
 The reference had only print() (chronos_sensor.py:100,108,143-155).  Exposed at GET /metrics:
-chains (requests) completed, verdict latency / TTFT histograms, generated tokens, engine step time, batch size,
-KV block usage.
+chains (requests) completed, verdict latency / TTFT histograms, generated tokens and tokens/s, engine step time,
+batch size, queue depth, KV block usage, and the engine's own counters (prefix-cache hit tokens, prefill / decode steps,
+decode row-steps, jumps, compactions, timeouts, cancellations) as ``chronos_engine_<name>_total``.  The engine never
+preempts (a request's KV blocks are reserved at admission), so ``chronos_preemptions_total`` stays 0 by design.
 """
 from __future__ import annotations
 
@@ -50,7 +52,9 @@ class Metrics:
         self.ttft = _Hist()
         self.step = _Hist()
         self.running = 0
+        self.waiting = 0
         self.kv_usage = 0.0
+        self.engine_stats: dict = {}
         self.t0 = time.time()
 
     def observe_request(self, r) -> None:
@@ -72,7 +76,11 @@ class Metrics:
         with self._lock:
             self.step.observe(seconds)
             self.running = len(engine.running)
+            self.waiting = len(engine.waiting) + len(getattr(engine, "prefilling", ()))
             self.kv_usage = engine.blocks.usage()
+            stats = getattr(engine, "stats", None)
+            if stats:
+                self.engine_stats = {k: v for k, v in stats.items() if isinstance(v, (int, float))}
 
     def render(self) -> str:
         with self._lock:
@@ -83,12 +91,19 @@ class Metrics:
                 "# TYPE chronos_generated_tokens_total counter", f"chronos_generated_tokens_total {self.gen_tokens}",
                 "# TYPE chronos_prompt_tokens_total counter", f"chronos_prompt_tokens_total {self.prompt_tokens}",
                 "# TYPE chronos_chains_per_second gauge", f"chronos_chains_per_second {self.requests / up}",
+                "# TYPE chronos_generated_tokens_per_second gauge",
+                f"chronos_generated_tokens_per_second {self.gen_tokens / up}",
                 "# TYPE chronos_running_sequences gauge", f"chronos_running_sequences {self.running}",
+                "# TYPE chronos_queued_requests gauge", f"chronos_queued_requests {self.waiting}",
+                "# TYPE chronos_preemptions_total counter", "chronos_preemptions_total 0",
                 "# TYPE chronos_kv_usage_ratio gauge", f"chronos_kv_usage_ratio {self.kv_usage}",
                 "# TYPE chronos_verdict_latency_seconds histogram", *self.latency.lines("chronos_verdict_latency_seconds"),
                 "# TYPE chronos_ttft_seconds histogram", *self.ttft.lines("chronos_ttft_seconds"),
                 "# TYPE chronos_engine_step_seconds histogram", *self.step.lines("chronos_engine_step_seconds"),
             ]
+            for k in sorted(self.engine_stats):
+                name = "chronos_engine_" + "".join(c if c.isalnum() else "_" for c in k) + "_total"
+                lines += [f"# TYPE {name} counter", f"{name} {self.engine_stats[k]}"]
         return "\n".join(lines) + "\n"
 
 

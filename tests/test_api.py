@@ -111,7 +111,10 @@ def test_streaming_and_endpoints(fake):
     assert "version" in requests.get(f"{fake.url}/api/version", timeout=5).json()
     assert requests.get(f"{fake.url}/", timeout=5).text == "Ollama is running"
     assert requests.get(f"{fake.url}/healthz", timeout=5).json()["status"] == "ok"
-    assert "chronos_requests_total" in requests.get(f"{fake.url}/metrics", timeout=5).text
+    metrics = requests.get(f"{fake.url}/metrics", timeout=5).text
+    for name in ("chronos_requests_total", "chronos_queued_requests", "chronos_generated_tokens_per_second",
+                 "chronos_preemptions_total 0", "chronos_verdict_latency_seconds_bucket"):
+        assert name in metrics
     bad = requests.post(f"{fake.url}/api/generate", json={"prompt": "x", "format": 7}, timeout=5)
     assert bad.status_code == 400
     bad = requests.post(f"{fake.url}/api/generate", data=b"{not json", timeout=5)
