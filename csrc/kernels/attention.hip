@@ -350,12 +350,19 @@ constexpr float kRescaleThrD = 8.f;  // decode LEAN defer-max threshold (log2 un
 
 // OCC: minimum workgroups per CU the register allocation must allow (3 = 3 waves per SIMD, <= 168 VGPRs: this
 // kernel is bound by K/V load latency, so more waves in flight is more bytes in flight; 1 = unconstrained)
-template <bool FP8, bool PF, bool LEAN, int OCC>
+//
+// RP (bf16 KV only): RoPE + paged-KV write fused in (the wave's decode step without rope_kv_write).  q is then the
+// raw [B, hq + 2 hkv, 128] QKV projection; the wave applies RoPE to its query rows in registers (every lane holds
+// both halves of its rotate-half pairs: dims 8 h4 + 32 c with c and c + 2) and writes the new token's (position
+// pos[seq], the last of the context) roped K and V into the cache before walking the context.
+template <bool FP8, bool PF, bool LEAN, int OCC, bool RP = false>
 __global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
     const uint16_t* __restrict__ q, const void* __restrict__ kcv, const void* __restrict__ vcv,
     const int32_t* __restrict__ block_table, int bt_stride, const int32_t* __restrict__ ctx_len,
     uint16_t* __restrict__ out, int nitems, int hq, int hkv, float scale_log2, float k_scale, float v_scale,
-    const int32_t* __restrict__ gst, int gn) {
+    const int32_t* __restrict__ gst, int gn, const int32_t* __restrict__ pos = nullptr,
+    const float* __restrict__ cos_sin = nullptr) {
+    static_assert(!(RP && FP8), "fused RoPE / KV write: bf16 KV only");
     constexpr int block_size = 16;
     if (gate_closed(gst, gn)) return;  // the engine's page size; compile-time so every K/V address is base + immediate
     const int lane = threadIdx.x & 63;
@@ -373,15 +380,60 @@ __global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
     int win = 0;
     int btv = lane < nblk ? bt[lane] : 0;
 
+    const int nh = hq + 2 * hkv;  // RP: heads per token row of the QKV projection
+    const int pnew = RP ? pos[seq] : 0;
+    const float* cs = RP ? cos_sin + (int64_t)pnew * kD : nullptr;
+    // rotate-half RoPE of one lane's 32 dims (chunks c = 0..3 at 8 h4 + 32 c; pairs (0, 2) and (1, 3)), rounded to
+    // bf16 exactly as rope_kv_write_kernel does
+    auto rope4 = [&](bf16x8 (&x)[4]) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const int d0 = 32 * c + 8 * h4;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float co = cs[d0 + j], si = cs[64 + d0 + j];
+                const float x1 = (float)x[c][j], x2 = (float)x[c + 2][j];
+                x[c][j] = (__bf16)(x1 * co - x2 * si);
+                x[c + 2][j] = (__bf16)(x2 * co + x1 * si);
+            }
+        }
+    };
+
     bf16x8 qf[4];
     {
         const bool valid = r < G;
-        const uint16_t* qp = q + ((int64_t)seq * hq + h * G + (valid ? r : 0)) * kD + 8 * h4;
+        const uint16_t* qp = RP ? q + ((int64_t)seq * nh + h * G + (valid ? r : 0)) * kD + 8 * h4
+                                : q + ((int64_t)seq * hq + h * G + (valid ? r : 0)) * kD + 8 * h4;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             bf16x8 v = *reinterpret_cast<const bf16x8*>(qp + 32 * c);
             if (!valid) v = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
             qf[c] = v;
+        }
+        if constexpr (RP) rope4(qf);
+    }
+    if constexpr (RP) {
+        // The new token's K (roped) and V go to the cache before the loop.  Each element is written by the very lane
+        // that later loads it (K: lane (r = slot, h4); V^T: lane (r, h4 = slot / 4)), so same-thread ordering makes
+        // the loop read the fresh values; no other wave touches this sequence's private last block.
+        const int tn = pnew & (block_size - 1);
+        const int64_t blkn = bt[pnew / block_size];
+        const uint16_t* row = q + (int64_t)seq * nh * kD;
+        if (r == tn) {
+            const uint16_t* kr = row + (int64_t)(hq + h) * kD + 8 * h4;
+            bf16x8 kn[4];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) kn[c] = *reinterpret_cast<const bf16x8*>(kr + 32 * c);
+            rope4(kn);
+            uint16_t* kdst = const_cast<uint16_t*>(kc) + (((blkn * hkv + h) * block_size) + tn) * kD + 8 * h4;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) *reinterpret_cast<bf16x8*>(kdst + 32 * c) = kn[c];
+        }
+        if (h4 == (tn >> 2)) {
+            const uint16_t* vr = row + (int64_t)(hq + hkv + h) * kD + r;
+            uint16_t* vdst = const_cast<uint16_t*>(vc) + ((blkn * hkv + h) * kD) * (int64_t)block_size + tn;
+#pragma unroll
+            for (int dt = 0; dt < 8; ++dt) vdst[(int64_t)(dt * 16 + r) * block_size] = vr[16 * dt];
         }
     }
 
@@ -558,6 +610,27 @@ __global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
             *reinterpret_cast<u16x4*>(op + 16 * dt) = ov;
         }
     }
+}
+
+// Fused decode step (RP): RoPE + paged-KV write + one-wave-per-(seq, kv head) attention.  Returns false (nothing
+// launched) off the shapes the one-wave kernel serves; the caller then runs rope_kv_write + launch_paged_attn.
+bool launch_decode_attn_rope(const uint16_t* qkv, const int32_t* pos, const float* cos_sin, void* kc, void* vc,
+                             const int32_t* block_table, int bt_stride, const int32_t* ctx_len, uint16_t* out, int n,
+                             int hq, int hkv, int block_size, float scale, hipStream_t st) {
+    const int nitems = n * hkv;
+    if (n == 0 || hq / hkv > 16 || block_size != 16 || nitems < 2048 || knob("decode_attn_legacy", 0) ||
+        knob("decode_pf", 0) || !knob("decode_lean", 1) || !knob("decode_rope_fused", 1))
+        return false;
+    const float scale_log2 = scale * 1.4426950408889634f;
+    if (knob("decode_occ3", 1))
+        hipLaunchKernelGGL((paged_decode_kernel<false, false, true, 3, true>), dim3((nitems + 3) / 4), dim3(256), 0,
+                           st, qkv, kc, vc, block_table, bt_stride, ctx_len, out, nitems, hq, hkv, scale_log2, 1.f,
+                           1.f, CHRONOS_GATE, pos, cos_sin);
+    else
+        hipLaunchKernelGGL((paged_decode_kernel<false, false, true, 1, true>), dim3((nitems + 3) / 4), dim3(256), 0,
+                           st, qkv, kc, vc, block_table, bt_stride, ctx_len, out, nitems, hq, hkv, scale_log2, 1.f,
+                           1.f, CHRONOS_GATE, pos, cos_sin);
+    return true;
 }
 
 // Split-completion tickets for the in-launch combine: one zeroed int per (tile, kv head), per device, allocated once by

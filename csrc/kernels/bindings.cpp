@@ -28,6 +28,8 @@ void launch_rope_kv_write(const uint16_t*, const int32_t*, const int32_t*, const
                           uint16_t*, void*, void*, int, int, int, int, int, bool, float, float, hipStream_t);
 void launch_silu_mul(const uint16_t*, uint16_t*, int64_t, int, hipStream_t);
 size_t paged_attn_smem(int nqt);
+bool launch_decode_attn_rope(const uint16_t*, const int32_t*, const float*, void*, void*, const int32_t*, int,
+                             const int32_t*, uint16_t*, int, int, int, int, float, hipStream_t);
 void launch_paged_attn(const uint16_t*, const void*, const void*, const int32_t*, int, const int32_t*,
                        const int32_t*, const int32_t*, int, int, int, uint16_t*, float*, float*, int, int, int, float,
                        bool, float, float, hipStream_t);
@@ -186,6 +188,37 @@ void rope_kv_write(const Tensor& qkv, const Tensor& pos, const Tensor& tok_seq, 
                                   cos_sin.data_ptr<float>(), bfm(q_out), k_cache.data_ptr(), v_cache.data_ptr(), (int)t,
                                   (int)hq, (int)hkv, (int)k_cache.size(2), write_q ? 1 : 0, fp8, (float)k_scale,
                                   (float)v_scale, cur_stream());
+}
+
+// Decode step attention with RoPE + paged-KV write fused in (attention.hip paged_decode_kernel<..., RP = true>).
+// Returns the [n, hq, 128] attention output, or an empty tensor when the fused kernel does not serve this shape (the
+// caller then runs rope_kv_write + paged_attention).  Decode rows only: row i is sequence i, its one token at pos[i]
+// is the last of its context (ctx_len[i] == pos[i] + 1).
+Tensor decode_attention_rope(const Tensor& qkv, const Tensor& pos, const Tensor& cos_sin, const Tensor& k_cache,
+                             const Tensor& v_cache, const Tensor& block_table, const Tensor& ctx_len, int64_t n,
+                             int64_t hq, double scale) {
+    chk_bf16(qkv, "qkv");
+    chk_i32(pos, "pos");
+    chk_i32(block_table, "block_table");
+    chk_i32(ctx_len, "ctx_len");
+    chk_gpu(cos_sin, "cos_sin");
+    CHK(cos_sin.scalar_type() == at::kFloat && cos_sin.dim() == 2 && cos_sin.size(1) == 128, "cos_sin [P,128] f32");
+    const bool fp8 = chk_kv(k_cache, v_cache);
+    const int64_t hkv = k_cache.size(1), bs = k_cache.size(2);
+    CHK(qkv.dim() == 2 && qkv.size(0) >= n && qkv.size(1) == (hq + 2 * hkv) * 128, "qkv must be [>=n, (hq+2hkv)*128]");
+    CHK(pos.numel() >= n && ctx_len.numel() >= n && block_table.dim() == 2 && block_table.size(0) >= n,
+        "pos / ctx_len / block_table need n rows");
+    CHK(hq % hkv == 0 && 16 % (hq / hkv) == 0, "GQA group Hq/Hkv must divide 16");
+    CHK(k_cache.dim() == 4 && k_cache.size(3) == 128 && v_cache.size(2) == 128 && v_cache.size(3) == bs,
+        "k_cache [NB, hkv, BS, 128], v_cache [NB, hkv, 128, BS]");
+    c10::hip::HIPGuardMasqueradingAsCUDA g(qkv.device());
+    if (fp8) return at::empty({0}, qkv.options());
+    auto out = at::empty({n, hq, 128}, qkv.options());
+    if (!chronos::launch_decode_attn_rope(bf(qkv), i32(pos), cos_sin.data_ptr<float>(), k_cache.data_ptr(),
+                                          v_cache.data_ptr(), i32(block_table), (int)block_table.size(1), i32(ctx_len),
+                                          bfm(out), (int)n, (int)hq, (int)hkv, (int)bs, (float)scale, cur_stream()))
+        return at::empty({0}, qkv.options());
+    return out;
 }
 
 Tensor silu_mul(const Tensor& gu) {
@@ -575,6 +608,8 @@ TORCH_LIBRARY(chronos, m) {
     m.def("ar_error(int h) -> int", &ar_error);
     m.def("ar_capacity(int h) -> int", &ar_capacity);
     m.def("ar_destroy(int h) -> ()", &ar_destroy);
+    m.def("decode_attention_rope(Tensor qkv, Tensor pos, Tensor cos_sin, Tensor(a!) k_cache, Tensor(b!) v_cache, "
+          "Tensor block_table, Tensor ctx_len, int n, int hq, float scale) -> Tensor");
     m.def("paged_attention(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_table, Tensor q_start, "
           "Tensor ctx_len, Tensor? tiles, int ntiles, int nqt, int nsplit, float scale, float k_scale=1.0, "
           "float v_scale=1.0) -> Tensor");
@@ -598,6 +633,7 @@ TORCH_LIBRARY_IMPL(chronos, CUDA, m) {
     m.impl("quant_rows", &quant_rows);
     m.impl("qlinear", &qlinear);
     m.impl("paged_attention", &paged_attention);
+    m.impl("decode_attention_rope", &decode_attention_rope);
     m.impl("constrained_sample", &constrained_sample);
     m.impl("ar_all_reduce", &ar_all_reduce);
     m.impl("ar_all_reduce_norm", &ar_all_reduce_norm);

@@ -29,6 +29,8 @@ from ..parallel.tp import TPContext
 # GEMV's prologue, RoPE + paged-KV write in the QKV GEMV's epilogue (CHRONOS_FUSE_NORM=0: the separate kernels)
 _FUSE_NORM = os.environ.get("CHRONOS_FUSE_NORM", "1") != "0"
 _FUSE_AR_NORM = os.environ.get("CHRONOS_FUSE_AR_NORM", "1") != "0"  # TP: fused IPC all-reduce + residual + RMSNorm
+# batched decode (>= 2048 (row, kv head) items, bf16 KV): RoPE + paged-KV write fused into the decode attention
+_FUSE_DECODE_ROPE = os.environ.get("CHRONOS_FUSE_DECODE_ROPE", "1") != "0"
 
 
 @dataclass
@@ -580,6 +582,7 @@ class LlamaModel:
     def _attn(self, li: int, lw: LayerWeights, st: dict, kv: KVCache) -> torch.Tensor:
         """Attention block up to the row-parallel o_proj; returns this rank's partial sum."""
         sb, T, x = st["sb"], st["T"], st["x"]
+        attn = None
         if (not self.w.fp8 and _FUSE_NORM and ops.qkv_rope(
                 x, lw.wqkv, sb.pos, sb.tok_seq, sb.block_table, self.cos_sin, st["q_buf"], kv.k[li], kv.v[li],
                 self.hq, self.hkv, kv.k_scale[li], kv.v_scale[li])):
@@ -587,16 +590,23 @@ class LlamaModel:
         else:
             x = ops.LazyNorm.force(x)
             qkv = ops.qlinear(*x, lw.wqkv.q, lw.wqkv.s) if self.w.fp8 else ops.linear(x, lw.wqkv)
-            ops.rope_kv_write(qkv, sb.pos, sb.tok_seq, sb.block_table, self.cos_sin, st["q_buf"], kv.k[li], kv.v[li],
-                              self.hq, self.hkv, True, kv.k_scale[li], kv.v_scale[li])
+            if _FUSE_DECODE_ROPE and sb.tiles is None and sb.cp is None and sb.nqt == 1 and sb.nsplit == 1:
+                # batched decode: RoPE + KV write inside the one-wave decode attention (None off its shapes)
+                attn = ops.decode_attention_rope(qkv, sb.pos, self.cos_sin, kv.k[li], kv.v[li], sb.block_table,
+                                                 sb.ctx_len, T, self.hq, self.scale)
+            if attn is None:
+                ops.rope_kv_write(qkv, sb.pos, sb.tok_seq, sb.block_table, self.cos_sin, st["q_buf"], kv.k[li],
+                                  kv.v[li], self.hq, self.hkv, True, kv.k_scale[li], kv.v_scale[li])
             if sb.cp is not None:  # CP: every rank writes the whole chunk's K/V before any rank attends
                 from ..parallel.context_parallel import gather_kv
 
                 cp = sb.cp
                 ops.rope_kv_write(gather_kv(qkv, self.hq, cp), cp.pos_all, cp.seq_all, cp.bt, self.cos_sin,
                                   cp.dummy_q, kv.k[li], kv.v[li], 0, self.hkv, False, kv.k_scale[li], kv.v_scale[li])
-        attn = ops.paged_attention(st["q_buf"], kv.k[li], kv.v[li], sb.block_table, sb.q_start, sb.ctx_len, sb.tiles,
-                                   sb.ntiles, sb.nqt, sb.nsplit, self.scale, kv.k_scale[li], kv.v_scale[li])
+        if attn is None:
+            attn = ops.paged_attention(st["q_buf"], kv.k[li], kv.v[li], sb.block_table, sb.q_start, sb.ctx_len,
+                                       sb.tiles, sb.ntiles, sb.nqt, sb.nsplit, self.scale, kv.k_scale[li],
+                                       kv.v_scale[li])
         if self.w.fp8:
             return ops.qlinear(*ops.quant_rows(attn.view(T, -1)), lw.wo.q, lw.wo.s)
         return self._out_proj(attn.view(T, -1), lw.wo, st)

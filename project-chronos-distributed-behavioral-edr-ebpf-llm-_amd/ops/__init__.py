@@ -212,6 +212,23 @@ def paged_attention(q, k_cache, v_cache, block_table, q_start, ctx_len, tiles=No
                                k_scale, v_scale)
 
 
+def decode_attention_rope(qkv, pos, cos_sin, k_cache, v_cache, block_table, ctx_len, n: int, hq: int,
+                          scale: float):
+    """Decode step (row i = sequence i, one token at pos[i], ctx_len[i] == pos[i] + 1): RoPE + paged-KV write + paged
+    attention in one launch (csrc/kernels/attention.hip paged_decode_kernel RP).  Returns the [n, hq, 128] output, or
+    None when the fused kernel does not serve the shape (fp8 KV, < 2048 (row, kv head) items, ...): the caller then
+    runs rope_kv_write + paged_attention, which compute the same thing."""
+    if not qkv.is_cuda:
+        return None
+    if _checking(qkv):
+        p, c = pos[:n].cpu().long(), ctx_len[:n].cpu().long()
+        _need(bool((c == p + 1).all()), "decode_attention_rope: ctx_len must be pos + 1 (decode rows)")
+        _need(bool(((p >= 0) & (p < cos_sin.shape[0])).all()), "decode_attention_rope: position outside the rope table")
+        _check_paged(block_table, k_cache, torch.arange(n), c, "decode_attention_rope")
+    out = _k().decode_attention_rope(qkv, pos, cos_sin, k_cache, v_cache, block_table, ctx_len, n, hq, scale)
+    return out if out.numel() else None
+
+
 def constrained_sample(logits, row_of_slot, next_tab, dist, done_state: int, state, remaining, temperature, seed,
                        ids, pos, ctx, nout, out_tokens, topk=None, topp=None, jump=None) -> None:
     """``jump``: optional int8 [S] flags — a row whose sampled token leads into a flagged state is parked as state

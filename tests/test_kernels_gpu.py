@@ -180,6 +180,41 @@ def test_paged_attention_decode_one_wave_kernel(hq, hkv):
         C.set_knob("decode_pf", 0)
 
 
+@pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8)])
+def test_decode_attention_rope_fused_matches_unfused(hq, hkv):
+    """Batched decode step with RoPE + paged-KV write fused into the one-wave decode attention vs rope_kv_write +
+    paged_attention (and the fp32 reference): ragged contexts incl. a new token at every block offset and past the
+    64-entry block-table window; the caches must hold the same new K / V afterwards."""
+    from chronos import ops
+    from chronos.models.llama import get_config, rope_table
+    from chronos.ops import reference as ref
+
+    g = torch.Generator().manual_seed(hq + 5)
+    ctx_lens = torch.randint(1, 300, (270,), generator=g).tolist()
+    ctx_lens[:20] = [1, 2, 15, 16, 17, 31, 32, 33, 1024, 1025, 1100, 47, 48, 49, 63, 64, 65, 4, 8, 12]
+    B = len(ctx_lens)
+    _, k1, v1, bt, qs, ctx = _attn_case([1] * B, ctx_lens, hq, hkv, 16, seed=hq + 9)
+    gd = torch.Generator(device=DEV).manual_seed(hq)
+    qkv = (torch.randn(B, (hq + 2 * hkv) * 128, device=DEV, generator=gd) * 2).to(torch.bfloat16)
+    pos = (ctx - 1).to(torch.int32)
+    cs = rope_table(get_config("llama3.1-8b"), 2048, DEV)
+    tok = torch.arange(B, dtype=torch.int32, device=DEV)
+    k2, v2 = k1.clone(), v1.clone()
+    qb = torch.empty(B, hq, 128, device=DEV, dtype=torch.bfloat16)
+    ops.rope_kv_write(qkv, pos, tok, bt, cs, qb, k2, v2, hq, hkv, True)
+    exp = ops.paged_attention(qb, k2, v2, bt, qs, ctx, None, B, 1, 1)
+    want = ref.paged_attention(qb, k2, v2, bt, qs, ctx, None, B, 1, 1)
+    out = ops.decode_attention_rope(qkv, pos, cs, k1, v1, bt, ctx, B, hq, 1.0 / math.sqrt(128))
+    assert out is not None, "the fused kernel must serve >= 2048 (row, kv head) items"
+    torch.cuda.synchronize()
+    _close(k1, k2, 1e-2, 1e-2)  # RoPE rounding may differ by an fma contraction
+    assert torch.equal(v1, v2)
+    _close(out, exp, 2e-2, 2e-2)
+    _close(out, want, 2e-2, 2e-2)
+    # below the one-wave threshold the op declines and the caller runs the unfused pair
+    assert ops.decode_attention_rope(qkv, pos, cs, k1, v1, bt, ctx, 8, hq, 1.0 / math.sqrt(128)) is None
+
+
 def test_paged_attention_spike_rescale():
     """Force the online-softmax rescale: one key dominates late in a long context."""
     from chronos import ops
