@@ -48,6 +48,8 @@ def parse():
                     help="decode steps per burst once a >=128-row bucket has started to drain (0 = always --burst)")
     ap.add_argument("--no-graphs", action="store_true")
     ap.add_argument("--no-prefix-cache", action="store_true")
+    ap.add_argument("--no-partial-prefix", action="store_true",
+                    help="reuse only whole cached KV blocks (no copy of a partially matching block's computed slots)")
     ap.add_argument("--async-harvest", action="store_true")
     ap.add_argument("--prefill-ramp", type=int, default=2048, help="first prefill step after idle (0 = full chunks)")
     ap.add_argument("--no-jump-forward", action="store_true", help="decode grammar-forced runs token by token")
@@ -135,7 +137,8 @@ def main():
     cfg = EngineConfig(model=a.model, device=str(device), max_slots=a.streams, max_model_len=a.max_model_len,
                        default_num_predict=a.num_predict, decode_burst=a.burst, tail_burst=a.tail_burst,
                        use_graphs=not a.no_graphs,
-                       prefix_cache=not a.no_prefix_cache, async_harvest=a.async_harvest, seed=0,
+                       prefix_cache=not a.no_prefix_cache, partial_prefix=not a.no_partial_prefix,
+                       async_harvest=a.async_harvest, seed=0,
                        prefill_ramp=a.prefill_ramp, jump_forward=not a.no_jump_forward,
                        weight_dtype=a.weights, tp_sequence_parallel=a.sequence_parallel)
     # TP: the ranks of a replica submit the same chains in the same order and step the same deterministic scheduler,

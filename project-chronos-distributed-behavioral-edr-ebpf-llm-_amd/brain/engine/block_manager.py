@@ -8,6 +8,13 @@ request reuses
 the longest cached run of its prompt's full blocks (refcounted, read-only) and prefills only the remainder.  Blocks
 whose refcount drops to zero stay cached and are recycled least-recently-used when the free list runs dry.
 
+Partial blocks: a prompt whose next block matches a cached block (full, or the partial last block of another prompt)
+only for its first j < 16 tokens gets a fresh block with those j computed token slots copied in (``lookup_partial``;
+the engine batches the copies before its next prefill forward) and prefills from token j.  Without it every prompt
+recomputes up to 15 tokens of its shared prefix: the wave's prompts share ~47 of ~93 tokens, ending mid-block.
+A source qualifies only for slots a launched prefill has already written (``mark_computed``), so the stream-ordered
+copy reads finished K/V.
+
 Block 0 is reserved as a scratch block: empty decode slots point their block table at it, so a captured decode graph
 that always runs a fixed number of rows never writes into another sequence's KV.
 """
@@ -30,6 +37,10 @@ class BlockManager:
         self._by_hash: dict[bytes, int] = {}     # content digest -> block
         self._hash_of: dict[int, bytes] = {}     # block -> content digest
         self._evictable: "OrderedDict[int, None]" = OrderedDict()  # cached blocks with refcount 0 (LRU order)
+        # partial-block sources: parent digest -> blocks at that depth; block -> (parent digest, its prompt tokens,
+        # computed slots).  An entry lives while its block holds that content (dropped when the block is reused).
+        self._children: dict[bytes, list[int]] = {}
+        self._part: dict[int, list] = {}
         self.hits = 0
         self.lookups = 0
 
@@ -45,10 +56,12 @@ class BlockManager:
 
     def _take(self) -> int:
         if self._free:
-            return self._free.pop()
-        b, _ = self._evictable.popitem(last=False)  # least recently used cached block
-        h = self._hash_of.pop(b)
-        self._by_hash.pop(h, None)
+            b = self._free.pop()
+        else:
+            b, _ = self._evictable.popitem(last=False)  # least recently used cached block
+            h = self._hash_of.pop(b)
+            self._by_hash.pop(h, None)
+        self._part.pop(b, None)  # new content: no longer a partial-block source
         return b
 
     def alloc(self, n: int) -> list[int]:
@@ -69,6 +82,7 @@ class BlockManager:
             if b in self._hash_of:
                 self._evictable[b] = None
             else:
+                self._part.pop(b, None)
                 self._free.append(b)
 
     # ---- prefix cache ----------------------------------------------------------------------------------------------
@@ -114,13 +128,70 @@ class BlockManager:
             self._by_hash[h] = b
             self._hash_of[b] = h
 
+    def note_prompt(self, tokens: Sequence[int], blocks: Sequence[int], first: int = 0) -> None:
+        """Record blocks[first:] of a prompt as future partial-block sources (no slot computed yet)."""
+        if not self.prefix_cache:
+            return
+        bs = self.block_size
+        n = min(self.blocks_for(len(tokens)), len(blocks))
+        hs = [b""] + self._hashes(tokens, n - 1)
+        for d in range(first, n):
+            b = blocks[d]
+            if b in self._part:
+                continue
+            self._part[b] = [hs[d], tuple(tokens[d * bs:(d + 1) * bs]), 0]
+            self._children.setdefault(hs[d], []).append(b)
+
+    def mark_computed(self, blocks: Sequence[int], start: int, end: int) -> None:
+        """Token positions [start, end) of the sequence owning ``blocks`` now have their K/V written (in stream
+        order)."""
+        bs = self.block_size
+        for d in range(start // bs, min(len(blocks), (end + bs - 1) // bs)):
+            e = self._part.get(blocks[d])
+            if e is not None and max(0, start - d * bs) <= e[2]:  # keeps the computed slots contiguous from 0
+                e[2] = max(e[2], min(bs, end - d * bs))
+
+    def lookup_partial(self, tokens: Sequence[int], nfull: int, min_tokens: int = 2):
+        """After ``nfull`` shared full blocks: the computed block at depth ``nfull`` whose slots agree longest with
+        the prompt's next tokens -> (block, j), the block referenced for the caller (release it once copied);
+        None below ``min_tokens``.  Never the whole prompt: its last token is recomputed for the logits."""
+        if not self.prefix_cache:
+            return None
+        bs = self.block_size
+        parent = self._hashes(tokens, nfull)[-1] if nfull else b""
+        want = tokens[nfull * bs:(nfull + 1) * bs]
+        cap = min(len(want), len(tokens) - 1 - nfull * bs)
+        best, bj = None, min_tokens - 1
+        kids = self._children.get(parent, [])
+        live = [b for b in kids if b in self._part and self._part[b][0] == parent]
+        if len(live) != len(kids):
+            kids[:] = live  # drop blocks reused since they were noted
+        for b in live:
+            e = self._part[b]
+            lim = min(cap, e[2])
+            j = 0
+            toks = e[1]
+            while j < lim and j < len(toks) and toks[j] == want[j]:
+                j += 1
+            if j > bj:
+                best, bj = b, j
+        if best is None:
+            return None
+        if best in self._evictable:
+            del self._evictable[best]
+        self._ref[best] = self._ref.get(best, 0) + 1
+        return best, bj
+
     def clear_cache(self) -> None:
         """Forget every cached prefix (blocks still referenced keep their contents; idle cached blocks are freed)."""
         for b in list(self._evictable):
             self._free.append(b)
+            self._part.pop(b, None)
         self._evictable.clear()
         self._by_hash.clear()
         self._hash_of.clear()
+        self._children.clear()
+        self._part.clear()
 
     def usage(self) -> float:
         return 1.0 - self.free / (self.num_blocks - 1)

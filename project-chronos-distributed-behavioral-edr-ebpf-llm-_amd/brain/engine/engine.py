@@ -72,6 +72,7 @@ class EngineConfig:
     grammar_capacity: int = 2048
     max_string: int = 160          # default maxLength for schema strings without one (keeps verdicts short)
     prefix_cache: bool = True      # reuse KV blocks of identical prompt prefixes (the shared CHRONOS template head)
+    partial_prefix: bool = True    # ... and the computed leading slots of a partially matching block (copied in)
     kv_dtype: str = "bf16"         # "bf16" or "fp8" (OCP e4m3fn, per-layer scale: half the KV bytes, 2x tokens/GPU)
     weight_dtype: str = "bf16"     # "bf16" or "fp8": W8A8 e4m3 projections on the block-scaled MFMA (csrc/kernels/fp8.hip)
     kv_scale: float = 1.0          # fp8 KV scale (stored = value / scale)
@@ -234,6 +235,7 @@ class Engine:
         # ---- scheduling state ----
         self.waiting: collections.deque[Request] = collections.deque()
         self.prefilling: list[Request] = []
+        self._copies: list = []  # pending partial-prefix block copies (src, dst, request, start, j)
         self.running: dict[int, Request] = {}
         self.free_slots = list(range(S - 1, -1, -1))
         self._rid = itertools.count()
@@ -404,6 +406,7 @@ class Engine:
             self.waiting.clear()
             self._cancels = []
         self.prefilling = []
+        self._copies = []
         self.running = {}
         self._pending = None
         self._check_parked = False
@@ -471,8 +474,18 @@ class Engine:
                     self.blocks.release(shared)
                     break
                 self.waiting.popleft()
+                part = self.blocks.lookup_partial(req.prompt_ids, len(shared)) if self.cfg.partial_prefix else None
+                if part is not None and not self.blocks.can_alloc(nblk - len(shared)):
+                    self.blocks.release([part[0]])  # its reference took an evictable block out of the free pool
+                    part = None
                 req.blocks = shared + self.blocks.alloc(nblk - len(shared))
                 req.prefilled = len(shared) * self.blocks.block_size
+                self.blocks.note_prompt(req.prompt_ids, req.blocks, len(shared))
+                if part is not None:  # the first j slots of block len(shared) come from a computed block
+                    src, j = part
+                    self._copies.append((src, req.blocks[len(shared)], req, req.prefilled, j))
+                    req.prefilled += j
+                    self.stats["partial_prefix_tokens"] += j
                 self.stats["prefix_hit_tokens"] += req.prefilled
                 # Publish this prompt's full blocks right away: a request admitted later in this same round can
                 # share them even before they are computed, because prefill packs requests in admission order and
@@ -488,7 +501,21 @@ class Engine:
             self.s_bt[h2d(torch.tensor(slots, dtype=torch.int64), self.device)] = h2d(
                 torch.tensor(rows, dtype=torch.int32), self.device)
 
+    def _copy_partial_blocks(self) -> None:
+        """Batched copy of the partial-prefix source blocks into their new owners (every layer's K and V, whole
+        blocks: the slots past j are rewritten by the owner's prefill before any attention reads them)."""
+        jobs, self._copies = self._copies, []
+        src = h2d(torch.tensor([c[0] for c in jobs], dtype=torch.int64), self.device)
+        dst = h2d(torch.tensor([c[1] for c in jobs], dtype=torch.int64), self.device)
+        for cache in (*self.kv.k, *self.kv.v):
+            cache.index_copy_(0, dst, cache.index_select(0, src))
+        for s, d, req, start, j in jobs:
+            self.blocks.mark_computed(req.blocks, start, start + j)
+            self.blocks.release([s])
+
     def _prefill_step(self) -> None:
+        if self._copies:
+            self._copy_partial_blocks()
         budget = self._ramp
         self._ramp = min(4 * self._ramp, self._chunk)
         chunks, starts, bts, reqs = [], [], [], []
@@ -519,6 +546,7 @@ class Engine:
             logits = self.model.forward(sb, self.kv)
         done_rows, done_reqs = [], []
         for i, (req, ch) in enumerate(zip(reqs, chunks)):
+            self.blocks.mark_computed(req.blocks, req.prefilled, req.prefilled + len(ch))
             req.prefilled += len(ch)
             if req.prefilled == len(req.prompt_ids):
                 done_rows.append(i)

@@ -19,6 +19,50 @@ def test_block_manager_refcounts_and_lru():
     assert len(set(taken)) == 9 and bm.lookup(toks) == []
 
 
+def test_partial_block_lookup_uses_only_computed_slots():
+    bm = BlockManager(16, 4)
+    a_toks = [1, 2, 3, 4, 5, 6, 7, 8, 9, 10]       # 2 full blocks + 2 tokens
+    a = bm.alloc(3)
+    bm.register(a_toks, a)
+    bm.note_prompt(a_toks, a)
+    b_toks = [1, 2, 3, 4, 5, 6, 70, 80, 90, 100]    # shares block 0 and 2 slots of block 1
+    assert bm.lookup_partial(b_toks, 1) is None      # nothing computed yet
+    bm.mark_computed(a, 0, 10)
+    got = bm.lookup_partial(b_toks, 1)
+    assert got == (a[1], 2)
+    bm.release([got[0]])
+    c_toks = [1, 2, 3, 4, 5, 6, 7, 8, 9, 11, 12]   # block 2 matches 1 slot: below min_tokens
+    assert bm.lookup_partial(c_toks, 2) is None
+    assert bm.lookup_partial(c_toks, 2, min_tokens=1) == (a[2], 1)
+    d_toks = [1, 2, 3, 4, 5, 6, 7]                   # prompt ends inside the block: its last token is recomputed
+    assert bm.lookup_partial(d_toks, 1) == (a[1], 2)
+    bm.release(a)
+    bm.release([a[1], a[2]])                         # the partial last block is freed and stops being a source
+    assert bm.lookup_partial(c_toks, 2, min_tokens=1) is None
+
+
+@pytest.mark.parametrize("partial", [False, True])
+def test_engine_partial_prefix_same_outputs(partial):
+    """Prompts arriving after earlier ones were prefilled reuse computed slots of partially matching blocks."""
+    from chronos.brain.engine.engine import Engine, EngineConfig
+    from chronos.sensor.prompt import VERDICT_SCHEMA, build_prompt
+    from chronos.sensor.replay import synthetic_chains
+
+    chains = synthetic_chains(12, seed=11, native=False)
+    outs, stats = [], []
+    for pc in (False, True):
+        eng = Engine(EngineConfig(model="tiny", device="cpu", max_slots=16, max_model_len=384, use_graphs=False,
+                                  prefix_cache=pc, partial_prefix=partial, max_prefill_tokens=120, prefill_ramp=0,
+                                  jump_forward=False))
+        reqs = [eng.submit(build_prompt(c.history), fmt=VERDICT_SCHEMA, num_predict=20) for c in chains]
+        eng.run_until_idle()
+        outs.append([r.out_ids for r in reqs])
+        stats.append(dict(eng.stats))
+    assert outs[0] == outs[1]
+    if partial:
+        assert stats[1]["partial_prefix_tokens"] > 0
+
+
 @pytest.mark.parametrize("chunk", [200, 40])
 def test_engine_prefix_cache_same_outputs(chunk):
     from chronos.brain.engine.engine import Engine, EngineConfig
