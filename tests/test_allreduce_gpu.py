@@ -22,6 +22,26 @@ def _port():
     return p
 
 
+def _collect(q, ps, world, timeout):
+    """Results of the ranks that report within ``timeout`` s (a rank that raised reports before its peers stall in a
+    collective); stragglers are killed so a hang cannot keep pytest from exiting."""
+    import queue
+    import time
+
+    got, end = {}, time.monotonic() + timeout
+    while len(got) < world and time.monotonic() < end:
+        try:
+            r, res = q.get(timeout=max(0.1, end - time.monotonic()))
+            got[r] = res
+        except queue.Empty:
+            break
+    for p in ps:
+        p.join(timeout=20 if len(got) == world else 1)
+        if p.is_alive():
+            p.kill()
+    return got
+
+
 def _inputs(rank, step, n):
     g = torch.Generator().manual_seed(1000 * step + rank)
     return (torch.randn(n, generator=g) * (rank + 1)).to(torch.bfloat16)
@@ -115,7 +135,9 @@ def _worker(rank, world, port, q):
                 pass
         dist.barrier()
     except Exception as e:  # noqa: BLE001
-        res = {"ok": False, "msg": repr(e)}
+        import traceback
+
+        res = {"ok": False, "msg": repr(e) + "\n" + traceback.format_exc()[-3000:]}
     q.put((rank, res))
     dist.barrier()
     dist.destroy_process_group()
@@ -128,13 +150,11 @@ def test_ipc_allreduce_ranks_share_one_gpu(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q), daemon=True) for r in range(world)]
     for p in ps:
         p.start()
-    got = dict(q.get(timeout=100) for _ in range(world))
-    for p in ps:
-        p.join(timeout=60)
-    assert all(got[r]["ok"] for r in range(world)), got
+    got = _collect(q, ps, world, 100)
+    assert all(got.get(r, {}).get("ok") for r in range(world)), got
 
 
 def _engine_worker(rank, world, port, q):
@@ -154,6 +174,7 @@ def _engine_worker(rank, world, port, q):
     try:
         tp = TPContext.from_group()
         tp.enable_ipc_allreduce()
+        tp.ipc_allreduce.spin_limit = 200_000_000
         fused_calls = [0]
         inner = tp.fast_allreduce_norm
 
@@ -178,6 +199,8 @@ def _engine_worker(rank, world, port, q):
             cfg = EngineConfig(model="tiny", device="cuda", max_slots=4, max_model_len=384, use_graphs=False,
                                decode_burst=4, seed=0)
             eng = Engine(cfg, tp=tp)
+            # both ranks past their (lazy) start-up before the first IPC all-reduce spins on the peer
+            dist.barrier()
             reqs = [eng.submit(build_prompt(c), fmt=VERDICT_SCHEMA, num_predict=24) for c in chains]
             eng.run_until_idle()
             outs[fuse] = [r.out_ids for r in reqs]
@@ -187,7 +210,9 @@ def _engine_worker(rank, world, port, q):
         elif fused_calls[0] == 0:
             res = {"ok": False, "msg": "fused all-reduce + norm never ran"}
     except Exception as e:  # noqa: BLE001
-        res = {"ok": False, "msg": repr(e)}
+        import traceback
+
+        res = {"ok": False, "msg": repr(e) + "\n" + traceback.format_exc()[-3000:]}
     q.put((rank, res))
     dist.barrier()
     dist.destroy_process_group()
@@ -199,10 +224,8 @@ def test_tp2_engine_fused_allreduce_norm_matches_unfused():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    ps = [ctx.Process(target=_engine_worker, args=(r, 2, port, q)) for r in range(2)]
+    ps = [ctx.Process(target=_engine_worker, args=(r, 2, port, q), daemon=True) for r in range(2)]
     for p in ps:
         p.start()
-    got = dict(q.get(timeout=110) for _ in range(2))
-    for p in ps:
-        p.join(timeout=60)
-    assert got[0]["ok"] and got[1]["ok"], got
+    got = _collect(q, ps, 2, 100)
+    assert got.get(0, {}).get("ok") and got.get(1, {}).get("ok"), got
