@@ -41,6 +41,7 @@ class BlockManager:
         # computed slots).  An entry lives while its block holds that content (dropped when the block is reused).
         self._children: dict[bytes, list[int]] = {}
         self._part: dict[int, list] = {}
+        self._memo = None  # (tokens, len, digest chain) of the last prompt hashed
         self.hits = 0
         self.lookups = 0
 
@@ -90,12 +91,19 @@ class BlockManager:
         """Chained SHA-256 digests (parent digest || block token ids as int32).  Prompt tokens are partly
         attacker-controlled (argv paths in the telemetry), so the key must be collision-resistant: a 64-bit
         non-cryptographic hash collision would hand one prompt another prompt's KV block."""
+        # Admission asks for the same prompt's chain up to four times (lookup, lookup_partial, register,
+        # note_prompt): keep the last prompt's full chain (identity-checked, the object is held so its id stays
+        # unique).
+        m = self._memo
+        if m is not None and m[0] is tokens and m[1] == len(tokens) and len(m[2]) >= nblocks:
+            return m[2][:nblocks]
         hs, h = [], b""
         bs = self.block_size
-        for i in range(nblocks):
+        for i in range(max(nblocks, len(tokens) // bs)):
             h = hashlib.sha256(h + array("i", tokens[i * bs:(i + 1) * bs]).tobytes()).digest()
             hs.append(h)
-        return hs
+        self._memo = (tokens, len(tokens), hs)
+        return hs[:nblocks]
 
     def lookup(self, tokens: Sequence[int]) -> list[int]:
         """Longest run of cached full blocks at the start of `tokens` (never the whole prompt: the last token must be
