@@ -53,13 +53,42 @@ def _ext_suffix() -> str:
 
 
 def _hash(files: list[str], flags: list[str]) -> str:
+    """Build key: repo-relative source paths + contents + flags with the repo location masked, so a snapshot of the
+    tree at another path (the GPU box runs it from a scratch directory) keeps its prebuilt libraries instead of
+    recompiling them on first import."""
     h = hashlib.sha256()
-    for f in sorted(files):
-        h.update(f.encode())
+    for f in sorted(files, key=lambda x: os.path.relpath(x, REPO_DIR)):
+        h.update(os.path.relpath(f, REPO_DIR).encode())
         with open(f, "rb") as fh:
             h.update(fh.read())
-    h.update(" ".join(flags).encode())
+    h.update(" ".join(flags).replace(REPO_DIR, "<repo>").encode())
     return h.hexdigest()[:16]
+
+
+class _BuildLock:
+    """Inter-process lock around the stamp check + build: ranks of one job import the package at the same moment,
+    and two of them rebuilding one library would load each other's half-written files."""
+
+    def __init__(self, name: str):
+        self.path = os.path.join(PKG_DIR, f".{name}.build.lock")
+        self.fh = None
+
+    def __enter__(self):
+        import fcntl
+
+        try:
+            self.fh = open(self.path, "a")
+        except OSError:  # read-only tree: nothing can be rebuilt here anyway
+            return self
+        fcntl.flock(self.fh, fcntl.LOCK_EX)
+        return self
+
+    def __exit__(self, *exc):
+        if self.fh is not None:
+            import fcntl
+
+            fcntl.flock(self.fh, fcntl.LOCK_UN)
+            self.fh.close()
 
 
 def _deps(pattern_dirs: list[str]) -> list[str]:
@@ -79,6 +108,11 @@ def _run(cmd: list[str]) -> None:
 def _build(name: str, sources: list[str], compiler: list[str], cflags: list[str], ldflags: list[str],
            deps: list[str], force: bool = False, jobs: int = 8) -> str:
     """Compile `sources` in parallel into PKG_DIR/<name><EXT_SUFFIX> unless the stamp matches."""
+    with _BuildLock(name):
+        return _build_locked(name, sources, compiler, cflags, ldflags, deps, force, jobs)
+
+
+def _build_locked(name, sources, compiler, cflags, ldflags, deps, force, jobs) -> str:
     out = os.path.join(PKG_DIR, name + _ext_suffix())
     stamp = out + ".stamp"
     key = _hash(sources + deps, compiler + cflags + ldflags)
@@ -93,7 +127,7 @@ def _build(name: str, sources: list[str], compiler: list[str], cflags: list[str]
         futs = [ex.submit(_run, compiler + cflags + ["-c", s, "-o", o]) for s, o in zip(sources, objs)]
         for f in futs:
             f.result()
-    tmp = out + ".tmp"
+    tmp = f"{out}.{os.getpid()}.tmp"
     _run(compiler + ["-shared", "-o", tmp] + objs + ldflags)
     os.replace(tmp, out)
     with open(stamp, "w") as fh:
