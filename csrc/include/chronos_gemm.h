@@ -1,0 +1,29 @@
+// chronos_gemm.h — host/device interface of the batched projection GEMM family (csrc/kernels/gemm_pp.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace chronos {
+
+struct PPArgs {
+    const uint16_t* x;
+    const uint16_t* w;
+    uint16_t* y;            // output (kResid: the new residual stream s)
+    const uint16_t* resid;  // kResid input residual
+    float* part_out;        // kResid: [M, N / (BN/4)] partial sums of s^2
+    const float* part_in;   // NORMP: [M, nparts_in] producer partials
+    float* ws;              // split-K fp32 slabs, [tiles * splitk, BM * BN]
+    int32_t* cnt;           // split-K tickets, one per tile (zero between calls: the last arriver resets its own)
+    int M, N, K, F, nparts_in, splitk, kts;
+    float eps;
+    int ablate;  // timing-only diagnostics (knob pp_ablate): 1 skip loop DMA, 2 skip LDS reads, 4 skip MFMA, 8 nt weights
+};
+
+// epilogue modes
+enum : int { kPPPlain = 0, kPPSwiglu = 1, kPPResid = 2 };
+constexpr int kPPConfigs = 8;
+int gemm_pp_bm(int cfg);  // x rows per tile
+int gemm_pp_bn(int cfg);  // W rows per tile
+bool launch_gemm_pp(int cfg, int mode, bool normp, bool prio, const PPArgs& a, hipStream_t st);
+
+}  // namespace chronos

@@ -20,6 +20,7 @@
 #include <cstring>
 
 #include "chronos_gemv.h"
+#include "chronos_gemm.h"
 
 namespace chronos {
 void launch_embedding(const int32_t*, const uint16_t*, uint16_t*, int, int, int64_t, int64_t, hipStream_t);
@@ -34,7 +35,7 @@ void launch_paged_attn(const uint16_t*, const void*, const void*, const int32_t*
                        const int32_t*, const int32_t*, int, int, int, uint16_t*, float*, float*, int, int, int, float,
                        bool, float, float, hipStream_t);
 void launch_constrained_sample(const void*, bool, int64_t, const int32_t*, int, int, const int16_t*, const int16_t*,
-                               const int8_t*, int, int32_t*, int32_t*, const float*, const int32_t*, const int32_t*, const float*,
+                               const int16_t*, int, int32_t*, int32_t*, const float*, const int32_t*, const int32_t*, const float*,
                                int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, int, hipStream_t);
 void launch_gemv(const uint16_t*, int, int, const uint16_t*, int, uint16_t*, bool, hipStream_t);
 void attn_init();
@@ -331,11 +332,11 @@ void constrained_sample(const Tensor& logits, const c10::optional<Tensor>& row_o
         CHK(topp->scalar_type() == at::kFloat && topp->numel() >= n, "topp: f32, one entry per slot");
         pp = topp->data_ptr<float>();
     }
-    const int8_t* jp = nullptr;
+    const int16_t* jp = nullptr;
     if (jump.has_value()) {
         chk_gpu(*jump, "jump");
-        CHK(jump->scalar_type() == at::kChar && jump->numel() == next.size(0), "jump must be int8 [S]");
-        jp = jump->data_ptr<int8_t>();
+        CHK(jump->scalar_type() == at::kShort && jump->numel() == next.size(0), "jump must be int16 [S]");
+        jp = jump->data_ptr<int16_t>();
     }
     c10::hip::HIPGuardMasqueradingAsCUDA g(logits.device());
     chronos::launch_constrained_sample(logits.data_ptr(), logits.scalar_type() == at::kFloat, logits.stride(0), rp,
@@ -472,6 +473,75 @@ Tensor gemm(const Tensor& x, const Tensor& w, bool swiglu, int64_t stages) {
     return y;
 }
 
+// Batched projection GEMM family (gemm_pp.hip): y = x @ w.T with a fused epilogue, M >= 3.
+//   mode 0 plain (y [M, N]); 1 swiglu (w = [gate; up] [2F, K], y [M, F] = silu(x Wg^T) * (x Wu^T)); 2 resid (y = the
+//   new residual stream bf16(bf16(x @ w.T) + resid), second output = per-row partial sums of y^2 [M, N / (BN/4)]).
+//   part_in given (modes 0/1): x is the raw residual stream s and the folded input RMSNorm is applied as the per-row
+//   scale rsqrt(sum(part_in[m]) / K + eps).  cfg = tile config (gemm_pp_bm / gemm_pp_bn), splitk divides K / 64.
+std::tuple<Tensor, Tensor> gemm_pp(const Tensor& x, const Tensor& w, int64_t mode, int64_t cfg, int64_t splitk,
+                                   const c10::optional<Tensor>& resid, const c10::optional<Tensor>& part_in,
+                                   double eps, bool prio) {
+    chk_bf16(x, "x");
+    chk_bf16(w, "w");
+    const int64_t K = x.size(-1), M = x.numel() / K, N = w.size(0);
+    CHK(w.dim() == 2 && w.size(1) == K, "gemm_pp: w must be [N, K]");
+    CHK(cfg >= 0 && cfg < chronos::kPPConfigs, "gemm_pp: cfg");
+    CHK(mode >= 0 && mode <= 2, "gemm_pp: mode");
+    const int BM = chronos::gemm_pp_bm((int)cfg), BN = chronos::gemm_pp_bn((int)cfg);
+    CHK(M >= 1 && M < (1LL << 31) / BM && K % 64 == 0 && K <= (1 << 20) && N * K < (1LL << 40), "gemm_pp: size");
+    CHK(splitk >= 1 && (K / 64) % splitk == 0, "gemm_pp: splitk must divide K / 64");
+    CHK(N % BN == 0, "gemm_pp: N % BN == 0");
+    CHK(mode != 1 || (BN / 8) % 16 == 0, "gemm_pp: swiglu needs BN >= 128");
+    CHK(mode != 2 || !part_in.has_value(), "gemm_pp: resid mode has no norm prologue");
+    c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+    chronos::PPArgs a{};
+    a.x = bf(x);
+    a.w = bf(w);
+    a.M = (int)M;
+    a.N = (int)N;
+    a.K = (int)K;
+    a.F = (int)(N / 2);
+    a.splitk = (int)splitk;
+    a.kts = (int)(K / 64 / splitk);
+    a.eps = (float)eps;
+    a.ablate = chronos::knob("pp_ablate", 0);
+    Tensor y = at::empty({M, mode == 1 ? N / 2 : N}, x.options());
+    a.y = bfm(y);
+    Tensor part_out;
+    if (mode == 2) {
+        CHK(resid.has_value(), "gemm_pp: resid mode needs resid");
+        chk_bf16(*resid, "resid");
+        CHK(resid->numel() == M * N, "gemm_pp: resid must be [M, N]");
+        a.resid = bf(*resid);
+        part_out = at::empty({M, N / (BN / 4)}, x.options().dtype(at::kFloat));
+        a.part_out = part_out.data_ptr<float>();
+    }
+    if (part_in.has_value()) {
+        chk_gpu(*part_in, "part_in");
+        CHK(part_in->scalar_type() == at::kFloat && part_in->dim() == 2 && part_in->size(0) == M, "part_in [M, P] f32");
+        a.part_in = part_in->data_ptr<float>();
+        a.nparts_in = (int)part_in->size(1);
+    }
+    const int64_t tiles = ((M + BM - 1) / BM) * (mode == 1 ? (N / 2) / (BN / 2) : N / BN);
+    Tensor ws;
+    if (splitk > 1) {
+        ws = at::empty({tiles * splitk * BM * BN}, x.options().dtype(at::kFloat));
+        a.ws = ws.data_ptr<float>();
+        // tickets: one zeroed buffer per (device, stream); every call leaves it zeroed (the last arriver resets)
+        static std::mutex mu;
+        static std::unordered_map<int64_t, Tensor> cnts;
+        std::lock_guard<std::mutex> lk(mu);
+        const int64_t key = ((int64_t)x.get_device() << 48) ^ (int64_t)(intptr_t)cur_stream();
+        auto it = cnts.find(key);
+        if (it == cnts.end() || it->second.numel() < tiles)
+            it = cnts.insert_or_assign(key, at::zeros({std::max<int64_t>(tiles, 1 << 16)},
+                                                       x.options().dtype(at::kInt))).first;
+        a.cnt = it->second.data_ptr<int32_t>();
+    }
+    CHK(chronos::launch_gemm_pp((int)cfg, (int)mode, part_in.has_value(), prio, a, cur_stream()), "gemm_pp: launch");
+    return {y, part_out};
+}
+
 // ---- W8A8 fp8-e4m3 path (fp8.hip).  Quantised tensors travel as uint8 (OCP e4m3fn bytes) + fp32 scales.
 // mode 0: quant(x); 1: quant(rmsnorm(x) * w); 2: resid <- bf16(x + resid), quant(rmsnorm(resid) * w);
 // 3: x = [gate | up] rows of 2F, quant(silu(gate) * up)
@@ -590,6 +660,7 @@ TORCH_LIBRARY(chronos, m) {
     m.def("silu_mul(Tensor gate_up) -> Tensor");
     m.def("gemv(Tensor x, Tensor w, bool swiglu) -> Tensor");
     m.def("gemm(Tensor x, Tensor w, bool swiglu, int stages=3) -> Tensor");
+    m.def("gemm_pp(Tensor x, Tensor w, int mode, int cfg, int splitk, Tensor? resid, Tensor? part_in, float eps, bool prio) -> (Tensor, Tensor)");
     m.def("gemv_resid(Tensor x, Tensor w, Tensor resid_in, Tensor(a!) resid_out) -> Tensor");
     m.def("gemv_normp(Tensor s, Tensor part, float eps, Tensor w, bool swiglu) -> Tensor");
     m.def("qkv_rope(Tensor x, Tensor? part, float eps, Tensor w, Tensor pos, Tensor tok_seq, "
@@ -627,6 +698,7 @@ TORCH_LIBRARY_IMPL(chronos, CUDA, m) {
     m.impl("silu_mul", &silu_mul);
     m.impl("gemv", &gemv);
     m.impl("gemm", &gemm);
+    m.impl("gemm_pp", &gemm_pp);
     m.impl("gemv_resid", &gemv_resid);
     m.impl("gemv_normp", &gemv_normp);
     m.impl("qkv_rope", &qkv_rope);

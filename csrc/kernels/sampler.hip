@@ -13,8 +13,11 @@
 // ring — so a captured decode graph can be replayed for many steps with no host round trip.  Rows whose state is
 // DONE (or < 0: -1 = empty slot, <= -2 = parked) are left untouched.
 //
-// Jump-forward (optional `jump[S]` flags): when the sampled token leads into a state whose continuation the grammar
-// forces for several tokens (`, "verdict": "`), the row is parked as state -2 - s instead of s.  A parked row is not
+// Jump-forward (optional `jump[S]`): when the sampled token leads into a state whose continuation the grammar forces
+// for several tokens (`, "verdict": "`), the row is parked as state -2 - s instead of s — only if its remaining
+// budget can take the run: jump[s] is the budget a jump from s needs (run length + the grammar's shortest finish
+// after it, 0 = no run), so a row that could not be jumped keeps decoding instead of parking at every state of the
+// run and being refused each time.  A parked row is not
 // live for the sampler or the decode gate; the host harvests it, appends the forced tokens in one small prefill-mode
 // forward (brain/engine/engine.py Engine._jump) and resumes decoding after them.
 #include "chronos_hip.h"
@@ -46,7 +49,7 @@ __device__ __forceinline__ uint32_t ord_key(float x) {
 template <typename LT, bool VEC>
 __global__ void __launch_bounds__(1024) constrained_sample_kernel(
     const LT* __restrict__ logits, int64_t lstride, const int32_t* __restrict__ row_of_slot, int vocab,
-    const int16_t* __restrict__ next, const int16_t* __restrict__ dist, const int8_t* __restrict__ jump,
+    const int16_t* __restrict__ next, const int16_t* __restrict__ dist, const int16_t* __restrict__ jump,
     int done_state, int32_t* __restrict__ state,
     int32_t* __restrict__ remaining, const float* __restrict__ temperature, const int32_t* __restrict__ seed,
     const int32_t* __restrict__ topk, const float* __restrict__ topp,
@@ -248,7 +251,7 @@ __global__ void __launch_bounds__(1024) constrained_sample_kernel(
         if (n < max_out) out_tokens[(int64_t)slot * max_out + n] = besti;
         nout[slot] = n + 1;
         remaining[slot] = budget;
-        state[slot] = (jump && ns != done_state && jump[ns]) ? -2 - ns : ns;
+        state[slot] = (jump && ns != done_state && jump[ns] > 0 && budget >= jump[ns]) ? -2 - ns : ns;
         if (ns != done_state) {
             ids[slot] = besti;
             pos[slot] += 1;
@@ -258,13 +261,18 @@ __global__ void __launch_bounds__(1024) constrained_sample_kernel(
 }
 
 void launch_constrained_sample(const void* logits, bool logits_f32, int64_t lstride, const int32_t* row_of_slot,
-                               int nslots, int vocab, const int16_t* next, const int16_t* dist, const int8_t* jump,
+                               int nslots, int vocab, const int16_t* next, const int16_t* dist, const int16_t* jump,
                                int done_state,
                                int32_t* state, int32_t* remaining, const float* temperature, const int32_t* seed,
                                const int32_t* topk, const float* topp, int32_t* ids, int32_t* pos, int32_t* ctx,
                                int32_t* nout, int32_t* out_tokens, int max_out, hipStream_t st) {
     if (nslots == 0) return;
-    const bool vec = knob("sampler_vec", 1) != 0;
+    // the greedy fast path loads 16 B of each logits row and DFA row per lane: only for 16-B-aligned rows (a sliced or
+    // padded logits view with another row stride takes the scalar loop)
+    const size_t esz = logits_f32 ? 4 : 2;
+    const bool aligned = ((uintptr_t)logits % 16 == 0) && ((size_t)lstride * esz) % 16 == 0 &&
+                         ((uintptr_t)next % 16 == 0) && (vocab & 7) == 0;
+    const bool vec = knob("sampler_vec", 1) != 0 && aligned;
 #define CS_LAUNCH(LT, V)                                                                                        \
     hipLaunchKernelGGL((constrained_sample_kernel<LT, V>), dim3(nslots), dim3(1024), 0, st, (const LT*)logits, \
                        lstride, row_of_slot, vocab, next, dist, jump, done_state, state, remaining, temperature, seed,  \

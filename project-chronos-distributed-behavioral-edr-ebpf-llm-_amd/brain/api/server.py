@@ -17,6 +17,8 @@ import argparse
 import asyncio
 import json
 import logging
+import os
+import threading
 import time
 
 from aiohttp import web
@@ -215,8 +217,6 @@ def main(argv=None) -> int:
         if a.tp > 1 or a.cp > 1:
             if a.tp > 1 and a.cp > 1:
                 raise SystemExit("--tp and --cp are exclusive (CP ranks hold full weights)")
-            import os
-
             from ...parallel.tp import TPContext
             from ...parallel.tp_engine import TPEngine, init_tp
             from .service import LockstepService
@@ -233,7 +233,11 @@ def main(argv=None) -> int:
             if grp.rank != 0:
                 tpe.follower_loop()  # until the leader shuts down
                 return 0
-            backend = LockstepService(tpe, a.served_name)
+            def fatal(e):  # the group is out of lockstep: exit non-zero so the supervisor restarts every rank
+                log.error("lockstep group failed (%s); exiting so the group restarts", e)
+                threading.Timer(2.0, lambda: os._exit(3)).start()  # let /healthz answer 503 meanwhile
+
+            backend = LockstepService(tpe, a.served_name, on_fatal=fatal)
         elif a.dp > 1:
             from ...parallel.router import DPRouter
 

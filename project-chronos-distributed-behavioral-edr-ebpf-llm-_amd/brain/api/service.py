@@ -75,7 +75,7 @@ class EngineService:
                 for r in done:
                     METRICS.observe_request(r)
 
-    def _step_failed(self, e: BaseException, what: str) -> None:
+    def _step_failed(self, e: BaseException, what: str, backoff: bool = True) -> None:
         """A step raised: mark the service stalled (/healthz 503), answer every in-flight request with an error
         (done_reason 'error', so no HTTP caller waits for a reply that will never come), then back off before the
         next step so a persistent fault does not become a hot loop of tracebacks."""
@@ -90,7 +90,8 @@ class EngineService:
         failed = self.engine.fail_all(f"engine step failed: {self.last_error}")
         for r in failed:
             METRICS.observe_request(r)
-        self._stop.wait(min(self.fail_backoff_s * (2 ** min(self.failures - 1, 6)), 10.0))
+        if backoff:
+            self._stop.wait(min(self.fail_backoff_s * (2 ** min(self.failures - 1, 6)), 10.0))
 
     def _watch(self) -> None:
         while not self._stop.wait(min(1.0, self.step_deadline_s / 4)):
@@ -212,12 +213,28 @@ class LockstepService(EngineService):
     """The HTTP-facing service of a TP (or CP) group's leader rank: the same asyncio API and watchdog as
     EngineService, but requests enter the lockstep scheduler (parallel/tp_engine.py TPEngine) and the scheduler
     thread steps it continuously — an idle step is the followers' heartbeat (they block in the step's broadcast).
-    Incremental token streaming is not offered here: a stream=true request gets its text in one piece at the end."""
+    Incremental token streaming is not offered here: a stream=true request gets its text in one piece at the end.
 
-    def __init__(self, tpe, model_name: str = "llama3", step_deadline_s: float = 120.0, idle_s: float = 0.02):
+    A failed lockstep step is fatal for the group: the followers' engines did not see the leader's failure, so any
+    further step would pair the leader's collectives with different ones on the followers (RCCL hang or garbage).
+    The leader therefore stops stepping for good, answers every in-flight and later request with an error (the
+    reference's ERROR verdict path, chronos_sensor.py:121-122), and calls ``on_fatal`` — the server's default exits
+    the process non-zero, which closes the control group so the followers' pending broadcast fails and they exit too;
+    the supervisor restarts the whole group in fresh processes (never an exec from a process that touched the GPU)."""
+
+    def __init__(self, tpe, model_name: str = "llama3", step_deadline_s: float = 120.0, idle_s: float = 0.02,
+                 on_fatal=None):
         self.tpe = tpe
         self.idle_s = idle_s
+        self.broken = False
+        self.on_fatal = on_fatal
         super().__init__(tpe.engine, model_name, step_deadline_s)
+
+    def _error_req(self, ids, reason: str) -> Request:
+        r = Request(-1, list(ids), None, 0)
+        r.done_reason, r.error = "error", reason
+        r.meta["internal_error"] = True
+        return r
 
     def _loop(self) -> None:
         while not self._stop.is_set():
@@ -231,11 +248,8 @@ class LockstepService(EngineService):
             try:
                 done, _ = self.tpe.step()
             except Exception as e:
-                # The followers' state is unknown after a failed lockstep step; the leader answers its requests
-                # with errors (the group needs a restart — healthz stays 503).
-                self._step_failed(e, "lockstep step failed")
-                self.tpe.drop_callbacks()
-                continue
+                self._fatal(e)
+                return  # no further step and no stop broadcast: either would mismatch the followers' collectives
             self._step_t0 = None
             if busy:
                 METRICS.observe_step(time.perf_counter() - t, self.engine)
@@ -248,11 +262,31 @@ class LockstepService(EngineService):
         except Exception:  # noqa: BLE001 — shutting down
             pass
 
+    def _fatal(self, e: BaseException) -> None:
+        self.broken = True
+        self._step_failed(e, "lockstep step failed; the TP group must be restarted", backoff=False)
+        self.tpe.drop_callbacks()
+        while True:  # requests queued behind the failed step never reach the engine
+            try:
+                item = self._q.get_nowait()
+            except queue.Empty:
+                break
+            if item[0] == "submit":
+                item[3](self._error_req(item[2], f"lockstep group failed: {self.last_error}"))
+        if self.on_fatal is not None:
+            try:
+                self.on_fatal(e)
+            except Exception:  # noqa: BLE001
+                log.exception("on_fatal hook failed")
+
     def _handle(self, item) -> None:
         kind = item[0]
         if kind == "submit":
             _, params, ids, on_done, _on_tokens, handle = item
             if handle.get("cancelled"):
+                return
+            if self.broken:
+                on_done(self._error_req(ids, f"lockstep group failed: {self.last_error}"))
                 return
             handle["tag"] = self.tpe.submit(ids, fmt=params.format, num_predict=params.num_predict,
                                             temperature=params.temperature, seed=params.seed, callback=on_done,
@@ -261,6 +295,18 @@ class LockstepService(EngineService):
             tag = item[1].get("tag")
             if tag is not None:
                 self.tpe.cancel(tag)
+
+    async def generate(self, params: GenerateParams) -> Request:
+        if self.broken:  # the scheduler thread has stopped: answer at once
+            return self._error_req(self._ids(params), f"lockstep group failed: {self.last_error}")
+        return await super().generate(params)
+
+    def close(self) -> None:
+        if self.broken:  # the loop already returned without releasing the followers (they exit with the group)
+            self._stop.set()
+            self._watchdog.join(timeout=5)
+            return
+        super().close()
 
     async def generate_stream(self, params: GenerateParams) -> AsyncIterator[tuple[str, Optional[Request]]]:
         req = await self.generate(params)

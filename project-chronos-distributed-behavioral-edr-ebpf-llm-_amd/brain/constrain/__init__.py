@@ -54,7 +54,7 @@ class GrammarBank:
         self.dist = torch.full((capacity,), 32767, dtype=torch.int16, device=self.device)
         self.dist[DONE] = 0
         self.encode, self.jump_min = encode, jump_min
-        self.jump = torch.zeros((capacity,), dtype=torch.int8, device=self.device)
+        self.jump = torch.zeros((capacity,), dtype=torch.int16, device=self.device)  # budget a jump needs, 0 = none
         self.jumps: dict[int, tuple[tuple[int, ...], int]] = {}  # global state -> (forced tokens, state after them)
         self.used = 1
         self._host_dist: list[int] = [0]
@@ -125,7 +125,7 @@ class GrammarBank:
         nlive = live.sum(axis=1)
         eos = [e for e in self.stop_ids if 0 <= e < nxt.shape[1]]
         glob = lambda s: DONE if s == S else s + base  # noqa: E731
-        flags = []
+        flags, needs = [], []
         for q in range(S):
             data, cur = bytearray(), q
             while not dfa.accept[cur] and nlive[cur] == 1 and len(data) < 96:
@@ -156,8 +156,10 @@ class GrammarBank:
                 if run:
                     self.jumps[q + base] = (tuple(run), glob(st))
                     flags.append(q + base)
+                    needs.append(min(32767, len(run) + self.min_tokens(glob(st))))
         if flags:
-            self.jump[torch.tensor(flags, dtype=torch.int64).to(self.device)] = 1
+            self.jump[torch.tensor(flags, dtype=torch.int64).to(self.device)] = torch.tensor(
+                needs, dtype=torch.int16).to(self.device)
 
     # ---- host-side helpers (tests, CPU engine) -----------------------------------------------------------------
     def step(self, state: int, tok: int) -> int:

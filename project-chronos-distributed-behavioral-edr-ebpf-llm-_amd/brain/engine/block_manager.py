@@ -27,19 +27,22 @@ from typing import Sequence
 
 
 class BlockManager:
-    def __init__(self, num_blocks: int, block_size: int, prefix_cache: bool = True):
+    def __init__(self, num_blocks: int, block_size: int, prefix_cache: bool = True, partial_prefix: bool = True):
         if num_blocks < 2:
             raise ValueError("need at least 2 KV blocks (block 0 is scratch)")
         self.num_blocks, self.block_size = num_blocks, block_size
         self.prefix_cache = prefix_cache
+        self.partial_prefix = prefix_cache and partial_prefix
         self._free = list(range(num_blocks - 1, 0, -1))
         self._ref: dict[int, int] = {}
         self._by_hash: dict[bytes, int] = {}     # content digest -> block
         self._hash_of: dict[int, bytes] = {}     # block -> content digest
         self._evictable: "OrderedDict[int, None]" = OrderedDict()  # cached blocks with refcount 0 (LRU order)
         # partial-block sources: parent digest -> blocks at that depth; block -> (parent digest, its prompt tokens,
-        # computed slots).  An entry lives while its block holds that content (dropped when the block is reused).
-        self._children: dict[bytes, list[int]] = {}
+        # computed slots).  An entry lives while its block holds that content: _drop_part removes it from both maps
+        # when the block is reused or freed, so neither grows past the number of blocks (argv makes most parents
+        # unique per prompt, and such a parent is never looked up again).
+        self._children: dict[bytes, dict[int, None]] = {}
         self._part: dict[int, list] = {}
         self._memo = None  # (tokens, len, digest chain) of the last prompt hashed
         self.hits = 0
@@ -55,6 +58,15 @@ class BlockManager:
     def can_alloc(self, n: int) -> bool:
         return self.free >= n
 
+    def _drop_part(self, b: int) -> None:
+        e = self._part.pop(b, None)
+        if e is not None:
+            kids = self._children.get(e[0])
+            if kids is not None:
+                kids.pop(b, None)
+                if not kids:
+                    del self._children[e[0]]
+
     def _take(self) -> int:
         if self._free:
             b = self._free.pop()
@@ -62,7 +74,7 @@ class BlockManager:
             b, _ = self._evictable.popitem(last=False)  # least recently used cached block
             h = self._hash_of.pop(b)
             self._by_hash.pop(h, None)
-        self._part.pop(b, None)  # new content: no longer a partial-block source
+        self._drop_part(b)  # new content: no longer a partial-block source
         return b
 
     def alloc(self, n: int) -> list[int]:
@@ -83,7 +95,7 @@ class BlockManager:
             if b in self._hash_of:
                 self._evictable[b] = None
             else:
-                self._part.pop(b, None)
+                self._drop_part(b)
                 self._free.append(b)
 
     # ---- prefix cache ----------------------------------------------------------------------------------------------
@@ -138,7 +150,7 @@ class BlockManager:
 
     def note_prompt(self, tokens: Sequence[int], blocks: Sequence[int], first: int = 0) -> None:
         """Record blocks[first:] of a prompt as future partial-block sources (no slot computed yet)."""
-        if not self.prefix_cache:
+        if not self.partial_prefix:
             return
         bs = self.block_size
         n = min(self.blocks_for(len(tokens)), len(blocks))
@@ -148,7 +160,7 @@ class BlockManager:
             if b in self._part:
                 continue
             self._part[b] = [hs[d], tuple(tokens[d * bs:(d + 1) * bs]), 0]
-            self._children.setdefault(hs[d], []).append(b)
+            self._children.setdefault(hs[d], {})[b] = None
 
     def mark_computed(self, blocks: Sequence[int], start: int, end: int) -> None:
         """Token positions [start, end) of the sequence owning ``blocks`` now have their K/V written (in stream
@@ -163,18 +175,14 @@ class BlockManager:
         """After ``nfull`` shared full blocks: the computed block at depth ``nfull`` whose slots agree longest with
         the prompt's next tokens -> (block, j), the block referenced for the caller (release it once copied);
         None below ``min_tokens``.  Never the whole prompt: its last token is recomputed for the logits."""
-        if not self.prefix_cache:
+        if not self.partial_prefix:
             return None
         bs = self.block_size
         parent = self._hashes(tokens, nfull)[-1] if nfull else b""
         want = tokens[nfull * bs:(nfull + 1) * bs]
         cap = min(len(want), len(tokens) - 1 - nfull * bs)
         best, bj = None, min_tokens - 1
-        kids = self._children.get(parent, [])
-        live = [b for b in kids if b in self._part and self._part[b][0] == parent]
-        if len(live) != len(kids):
-            kids[:] = live  # drop blocks reused since they were noted
-        for b in live:
+        for b in self._children.get(parent, ()):
             e = self._part[b]
             lim = min(cap, e[2])
             j = 0
@@ -194,7 +202,6 @@ class BlockManager:
         """Forget every cached prefix (blocks still referenced keep their contents; idle cached blocks are freed)."""
         for b in list(self._evictable):
             self._free.append(b)
-            self._part.pop(b, None)
         self._evictable.clear()
         self._by_hash.clear()
         self._hash_of.clear()

@@ -213,7 +213,7 @@ class Engine:
                 dist.all_reduce(t, op=dist.ReduceOp.MIN, group=grp.group)
                 nb = int(t.item())
         self.kv = KVCache(mc, self.tp, nb, bs, self.device, cfg.kv_dtype, cfg.kv_scale, cfg.kv_scale)
-        self.blocks = BlockManager(nb, bs, prefix_cache=cfg.prefix_cache)
+        self.blocks = BlockManager(nb, bs, prefix_cache=cfg.prefix_cache, partial_prefix=cfg.partial_prefix)
         # ---- slot state (device) ----
         S, dev = cfg.max_slots, self.device
         i32 = dict(dtype=torch.int32, device=dev)
@@ -413,7 +413,7 @@ class Engine:
         S = self.cfg.max_slots
         self.free_slots = list(range(S - 1, -1, -1))
         self.blocks = BlockManager(self.blocks.num_blocks, self.blocks.block_size,
-                                   prefix_cache=self.blocks.prefix_cache)
+                                   prefix_cache=self.blocks.prefix_cache, partial_prefix=self.cfg.partial_prefix)
         try:
             self.s_state.fill_(-1)
             self.s_bt.zero_()
@@ -777,7 +777,9 @@ class Engine:
             n0, k = int(nout[s]), len(run)
             if not run or n0 > self.cfg.max_out or n0 + k > self.cfg.max_out or \
                     r.num_predict - n0 - k < self.bank.min_tokens(end):
+                # safety net only: the sampler parks a row only when its budget takes the run (GrammarBank.jump)
                 unpark.append((r.slot, state))
+                self.stats["jump_refused"] += 1
                 continue
             ids = outs[s, :n0].tolist() + list(run)
             r.meta.setdefault("jump_spans", []).append((n0, k))

@@ -224,7 +224,8 @@ def constrained_sample(logits, row_of_slot, next_tab, dist, done_state: int, sta
             out_tokens[slot, k] = tok
         nout[slot] = k + 1
         remaining[slot] = budget
-        state[slot] = -2 - ns if (jump is not None and ns != done_state and int(jump[ns])) else ns
+        park = jump is not None and ns != done_state and 0 < int(jump[ns]) <= budget
+        state[slot] = -2 - ns if park else ns
         if ns != done_state:
             ids[slot] = tok
             pos[slot] += 1

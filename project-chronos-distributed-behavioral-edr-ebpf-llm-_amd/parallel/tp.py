@@ -64,8 +64,10 @@ class TPContext:
             return None
 
         def fast_norm(x: torch.Tensor, resid: torch.Tensor, w: torch.Tensor, eps: float) -> Optional[torch.Tensor]:
+            # the fused kernel is one-shot (every rank reads all W peers' rows): messages the size policy sends to
+            # two-shot (mid-sized, W > 2) take the two-shot all-reduce + add_rmsnorm instead
             if (x.numel() * x.element_size() <= threshold and ar.fits(x) and x.dim() == 2 and x.is_contiguous()
-                    and resid.is_contiguous() and x.shape[1] % 8 == 0 and x.shape[1] <= 16384):
+                    and resid.is_contiguous() and x.shape[1] % 8 == 0 and x.shape[1] <= 16384 and ar.pick(x) == 1):
                 return ar.all_reduce_norm(x, resid, w, eps)
             return None
 

@@ -134,3 +134,84 @@ def test_jump_forward_gpu_graphs_teacher_forced():
     off.run_until_idle()
     assert off.stats["jumps"] == 0
     json.loads(r0.text)
+
+
+def _park_case(budget, need, dev="cpu"):
+    """States: 0 -(tok 1)-> 1 -(tok 2)-> DONE(=3 here); state 1 starts a forced run needing `need` budget."""
+    from chronos import ops
+
+    V, done = 4, 3
+    nxt = torch.full((4, V), -1, dtype=torch.int16)
+    nxt[0, 1], nxt[1, 2] = 1, done
+    dist = torch.tensor([2, 1, 32767, 0], dtype=torch.int16)
+    jump = torch.tensor([0, need, 0, 0], dtype=torch.int16)
+    i32 = lambda *v: torch.tensor(v, dtype=torch.int32, device=dev)  # noqa: E731
+    state, rem = i32(0), i32(budget + 1)  # the sampled token costs 1: `budget` is what is left after it
+    ids, pos, ctx, nout = i32(0), i32(5), i32(6), i32(0)
+    out = torch.zeros(1, 8, dtype=torch.int32, device=dev)
+    logits = torch.zeros(1, V, device=dev)
+    ops.constrained_sample(logits, None, nxt.to(dev), dist.to(dev), done, state, rem,
+                           torch.zeros(1, device=dev), i32(0), ids, pos, ctx, nout, out, None, None, jump.to(dev))
+    return int(state[0])
+
+
+def test_park_only_when_the_budget_takes_the_run():
+    """The sampler parks a row entering a forced-run state only if its remaining budget covers the run plus the
+    grammar's shortest finish after it (GrammarBank.jump); otherwise the row keeps decoding (a refused
+    jump used to re-park at every state of the run, one token per burst)."""
+    assert _park_case(budget=5, need=5) == -2 - 1
+    assert _park_case(budget=4, need=5) == 1
+    assert _park_case(budget=9, need=0) == 1
+
+
+@pytest.mark.gpu
+def test_park_only_when_the_budget_takes_the_run_gpu():
+    from chronos import ops
+
+    ops.load()
+    assert _park_case(budget=5, need=5, dev="cuda") == -2 - 1
+    assert _park_case(budget=4, need=5, dev="cuda") == 1
+
+
+def test_tight_budget_never_parks_a_row_it_cannot_jump(tok):
+    """num_predict at or just above the grammar's shortest verdict: a forced run the budget cannot take must not
+    park the row (it would be refused and unparked at every state of the run, one token per burst)."""
+    from chronos.sensor.prompt import VERDICT_SCHEMA
+
+    eng = _engine(tok, True)
+    cg = eng.bank.get(VERDICT_SCHEMA)
+    need = eng.bank.min_tokens(cg.start)
+    prompts = _prompts(2)
+    for extra in (0, 1, 2, 4):
+        reqs = [eng.submit(p, fmt=VERDICT_SCHEMA, num_predict=need + extra) for p in prompts]
+        eng.run_until_idle()
+        for r in reqs:
+            assert r.done_reason in ("stop", "length")
+            if r.done_reason == "stop":
+                assert set(json.loads(r.text)) == {"risk_score", "verdict", "reason"}
+    assert eng.stats["jump_refused"] == 0
+    eng2 = _engine(tok, True)
+    for r in [eng2.submit(p, fmt=VERDICT_SCHEMA, num_predict=40) for p in prompts]:
+        pass
+    eng2.run_until_idle()
+    assert eng2.stats["jumps"] > 0 and eng2.stats["jump_refused"] == 0
+
+
+@pytest.mark.gpu
+def test_sampler_greedy_on_padded_logits_view():
+    """A logits view whose row stride is not a multiple of 16 B must not take the 16-B vector path."""
+    from chronos import ops
+
+    ops.load()
+    V, n = 64, 3
+    g = torch.Generator(device="cuda").manual_seed(0)
+    base = torch.randn(n, V + 3, device="cuda", generator=g).to(torch.bfloat16)
+    logits = base[:, 1:V + 1]  # stride V + 3 elements, base offset 2 B: misaligned rows
+    nxt = torch.zeros(1, V, dtype=torch.int16, device="cuda")  # one looping state, every token legal
+    dist = torch.ones(1, dtype=torch.int16, device="cuda")
+    i32 = lambda v: torch.tensor(v, dtype=torch.int32, device="cuda")  # noqa: E731
+    state, rem = i32([0] * n), i32([10] * n)
+    out = torch.zeros(n, 4, dtype=torch.int32, device="cuda")
+    ops.constrained_sample(logits, None, nxt, dist, -5, state, rem, torch.zeros(n, device="cuda"), i32([0] * n),
+                           i32([0] * n), i32([0] * n), i32([1] * n), i32([0] * n), out)
+    assert out[:, 0].tolist() == logits.float().argmax(1).tolist()

@@ -41,6 +41,30 @@ def test_partial_block_lookup_uses_only_computed_slots():
     assert bm.lookup_partial(c_toks, 2, min_tokens=1) is None
 
 
+def test_partial_source_maps_stay_bounded():
+    """Unique prompts (argv makes deep parents unique) cycling through a small cache: the partial-block source maps
+    must shrink as blocks are reused or freed, never grow with the number of requests."""
+    import random
+
+    rng = random.Random(0)
+    bm = BlockManager(24, 4)
+    for i in range(400):
+        toks = [1, 2, 3, 4, 5, 6] + [rng.randrange(1000) for _ in range(rng.randrange(3, 15))]
+        shared = bm.lookup(toks)
+        blocks = shared + bm.alloc(bm.blocks_for(len(toks)) - len(shared))
+        bm.note_prompt(toks, blocks, len(shared))
+        bm.mark_computed(blocks, len(shared) * 4, len(toks))
+        bm.register(toks, blocks)
+        bm.release(blocks)
+        assert len(bm._part) <= bm.num_blocks
+        assert sum(len(v) for v in bm._children.values()) == len(bm._part)
+        assert len(bm._children) <= bm.num_blocks
+    off = BlockManager(8, 4, partial_prefix=False)
+    b = off.alloc(2)
+    off.note_prompt(list(range(8)), b)
+    assert not off._part and not off._children and off.lookup_partial(list(range(8)), 1) is None
+
+
 @pytest.mark.parametrize("partial", [False, True])
 def test_engine_partial_prefix_same_outputs(partial):
     """Prompts arriving after earlier ones were prefilled reuse computed slots of partially matching blocks."""
