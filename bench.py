@@ -16,6 +16,11 @@ long-running server).  The default remains the wave form above.
 
 Weights are random-init Llama-3-8B (real architecture, bf16, no checkpoint offline); data is synthetic telemetry.
 Work per GPU is fixed as N grows (weak scaling).  Rank 0 prints ONE JSON line.
+
+``--gpus N`` is authoritative: started without a launcher (no WORLD_SIZE) and N > 1, bench.py starts
+``torch.distributed.run --nproc-per-node N`` on itself as a CHILD process before anything touches the GPU (never an
+exec) and exits with its code; under a launcher, a WORLD_SIZE that differs from N, or N above the visible devices,
+is an error — a scaling point must never silently measure fewer GPUs than it reports.
 """
 from __future__ import annotations
 
@@ -107,8 +112,45 @@ def run_closed(a, eng, prompts, barrier, progress):
     return elapsed, done[n0:target], hits
 
 
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def ensure_world(a) -> int | None:
+    """Reconcile --gpus with the launch.  Returns an exit code when this process only supervised a self-launch (or
+    found a mismatch), None when it is a rank that should run the benchmark."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if a.device == "cuda":
+        visible = torch.cuda.device_count()  # counts devices without initialising HIP
+        if a.gpus > visible:
+            print(f"bench.py: --gpus {a.gpus} but only {visible} GPU(s) visible", file=sys.stderr)
+            return 2
+    if env_world is not None:
+        if int(env_world) != a.gpus:
+            print(f"bench.py: --gpus {a.gpus} disagrees with WORLD_SIZE {env_world}", file=sys.stderr)
+            return 2
+        return None
+    if a.gpus <= 1:
+        return None
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"[bench] launching {a.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+
+
 def main():
     a = parse()
+    rc = ensure_world(a)
+    if rc is not None:
+        return rc
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -272,4 +314,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -16,12 +16,12 @@ struct PPArgs {
     int32_t* cnt;           // split-K tickets, one per tile (zero between calls: the last arriver resets its own)
     int M, N, K, F, nparts_in, splitk, kts;
     float eps;
-    int ablate;  // timing-only diagnostics (knob pp_ablate): 1 skip loop DMA, 2 skip LDS reads, 4 skip MFMA, 8 nt weights
+    int ablate;  // timing-only diagnostics (knob pp_ablate): 1 skip loop DMA, 2 skip LDS reads, 4 skip MFMA, 8 nt weights, 16/32 alias every W/x tile onto tile 0
 };
 
 // epilogue modes
 enum : int { kPPPlain = 0, kPPSwiglu = 1, kPPResid = 2 };
-constexpr int kPPConfigs = 8;
+constexpr int kPPConfigs = 12;
 int gemm_pp_bm(int cfg);  // x rows per tile
 int gemm_pp_bn(int cfg);  // W rows per tile
 bool launch_gemm_pp(int cfg, int mode, bool normp, bool prio, const PPArgs& a, hipStream_t st);

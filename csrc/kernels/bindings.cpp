@@ -490,7 +490,7 @@ std::tuple<Tensor, Tensor> gemm_pp(const Tensor& x, const Tensor& w, int64_t mod
     const int BM = chronos::gemm_pp_bm((int)cfg), BN = chronos::gemm_pp_bn((int)cfg);
     CHK(M >= 1 && M < (1LL << 31) / BM && K % 64 == 0 && K <= (1 << 20) && N * K < (1LL << 40), "gemm_pp: size");
     CHK(splitk >= 1 && (K / 64) % splitk == 0, "gemm_pp: splitk must divide K / 64");
-    CHK(N % BN == 0, "gemm_pp: N % BN == 0");
+    CHK(mode == 0 ? N % 4 == 0 : N % BN == 0, "gemm_pp: N % 4 (plain) / N % BN (swiglu, resid)");
     CHK(mode != 1 || (BN / 8) % 16 == 0, "gemm_pp: swiglu needs BN >= 128");
     CHK(mode != 2 || !part_in.has_value(), "gemm_pp: resid mode has no norm prologue");
     c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
@@ -522,7 +522,7 @@ std::tuple<Tensor, Tensor> gemm_pp(const Tensor& x, const Tensor& w, int64_t mod
         a.part_in = part_in->data_ptr<float>();
         a.nparts_in = (int)part_in->size(1);
     }
-    const int64_t tiles = ((M + BM - 1) / BM) * (mode == 1 ? (N / 2) / (BN / 2) : N / BN);
+    const int64_t tiles = ((M + BM - 1) / BM) * (mode == 1 ? (N / 2) / (BN / 2) : (N + BN - 1) / BN);
     Tensor ws;
     if (splitk > 1) {
         ws = at::empty({tiles * splitk * BM * BN}, x.options().dtype(at::kFloat));

@@ -62,16 +62,23 @@ __device__ __forceinline__ void pp_bar() {
 // lane group land on 16 distinct 16-B slots)
 __device__ __forceinline__ int swz64(int row) { return (4 - ((row >> 2) & 3)) & 3; }
 
-template <int BM, int BN, int STAGES, bool HALF, int MODE, bool NORMP, bool PRIO>
+// SPLIT (HALF only): separate rings — group 0 DMAs only W into a DW-deep ring, group 1 only x into a DX-deep one.
+// s_waitcnt vmcnt retires a wave's loads in issue order, so with one shared ring the far-ahead prefetch of the cold
+// weight stream would have to complete as early as the near-ahead x tile; with one operand per wave group each
+// group's counted wait covers only its own operand and the W ring can run DW-1 chunks ahead.
+template <int BM, int BN, int STAGES, bool HALF, int MODE, bool NORMP, bool PRIO, int DW = STAGES, int DX = STAGES,
+          bool SPLIT = false>
 __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(PPArgs a) {
     constexpr int RB = HALF ? 64 : 128;                        // LDS row bytes (k per stage * 2)
     constexpr int RPI = 1024 / RB;                             // image rows per LDS-DMA instruction
     constexpr int WIMG = BN * RB, XIMG = BM * RB, STAGE = WIMG + XIMG;
-    constexpr int WI = BN / RPI / 8, XI = BM / RPI / 8;        // LDS-DMA instructions per wave per stage
+    // LDS-DMA instructions per wave per stage: all 8 waves share both operands, or (SPLIT) 4 waves per operand
+    constexpr int WI = SPLIT ? BN / RPI / 4 : BN / RPI / 8, XI = SPLIT ? BM / RPI / 4 : BM / RPI / 8;
     constexpr int NPER = WI + XI;
     constexpr int NT = BN / 64;                                // 16-row W tiles per wave
     constexpr int MT = BM / 32;                                // 16-row x tiles per wave
-    constexpr int EXTRA = STAGES * STAGE;                      // flag + inv[BM] after the ring
+    constexpr int EXTRA = SPLIT ? DW * WIMG + DX * XIMG : STAGES * STAGE;  // flag + inv[BM] after the ring(s)
+    static_assert(!SPLIT || (HALF && DW >= 2 && DX >= 2), "split rings: 32-deep stages, >= 2 buffers each");
     static_assert(WI >= 1 && XI >= 1, "tile too small for 8 loader waves");
     static_assert(MODE != kSwiglu || (BN / 8) % 16 == 0, "swiglu: BN/8 gate rows per wave, multiple of 16");
     extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
@@ -80,7 +87,7 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(PPArgs a) {
     const int g = __builtin_amdgcn_readfirstlane(wave >> 2), wj = wave & 3;
     const int M = a.M, K = a.K;
     const int mt = (M + BM - 1) / BM;
-    const int ntl = MODE == kSwiglu ? a.F / (BN / 2) : a.N / BN;
+    const int ntl = MODE == kSwiglu ? a.F / (BN / 2) : (a.N + BN - 1) / BN;
     const int S = a.splitk;
     const int task = xcd_remap(blockIdx.x, mt * ntl * S);
     const int ks = task % S, tile = task / S;
@@ -97,41 +104,60 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(PPArgs a) {
     };
     const uint16_t* wsrc[WI];
     const uint16_t* xsrc[XI];
+    const int wslot = SPLIT ? wj : wave;  // this wave's share of the DMA instructions of a stage
 #pragma unroll
     for (int i = 0; i < WI; ++i) {
-        const int r = (wave * WI + i) * RPI + lane / (RB / 16);
+        const int r = (wslot * WI + i) * RPI + lane / (RB / 16);
         int wrow;
+        const int tnw = (a.ablate & 16) ? 0 : tn;  // diagnostics: every W tile aliased onto tile 0 (L2-resident)
         if constexpr (MODE == kSwiglu)
-            wrow = r < BN / 2 ? tn * (BN / 2) + r : a.F + tn * (BN / 2) + (r - BN / 2);
+            wrow = r < BN / 2 ? tnw * (BN / 2) + r : a.F + tnw * (BN / 2) + (r - BN / 2);
         else
-            wrow = tn * BN + r;
+            wrow = min(tnw * BN + r, a.N - 1);  // a partial last W tile re-reads row N-1 (never stored)
         wsrc[i] = a.w + (int64_t)wrow * K + kbeg + src_chunk(r) * 8;
     }
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
-        const int r = (wave * XI + i) * RPI + lane / (RB / 16);
-        const int xr = min(m0 + r, M - 1);
+        const int r = (wslot * XI + i) * RPI + lane / (RB / 16);
+        const int xr = (a.ablate & 32) ? r % M : min(m0 + r, M - 1);  // diagnostics: x tiles aliased onto tile 0
         xsrc[i] = a.x + (int64_t)xr * K + kbeg + src_chunk(r) * 8;
     }
     const bool wnt = a.ablate & 8;
-    auto issue = [&](int j, int stg) {
-        unsigned char* st = smem + stg * STAGE;
+    // LDS images of stage (or, SPLIT, chunk) j
+    auto wbuf = [&](int j) -> unsigned char* {
+        if constexpr (SPLIT) return smem + (j % DW) * WIMG;
+        else return smem + (j % STAGES) * STAGE;
+    };
+    auto xbuf = [&](int j) -> unsigned char* {
+        if constexpr (SPLIT) return smem + DW * WIMG + (j % DX) * XIMG;
+        else return smem + (j % STAGES) * STAGE + WIMG;
+    };
+    auto issue_w = [&](int j) {
+        unsigned char* st = wbuf(j);
         const int koff = j * (RB / 2);
         if (wnt) {  // non-temporal policy on the streamed weights (knob pp_wnt)
 #pragma unroll
             for (int i = 0; i < WI; ++i)
                 __builtin_amdgcn_global_load_lds((gbl_ptr_t)(wsrc[i] + koff),
-                                                 (lds_ptr_t)(st + (wave * WI + i) * 1024), 16, 0, 2);
+                                                 (lds_ptr_t)(st + (wslot * WI + i) * 1024), 16, 0, 2);
         } else {
 #pragma unroll
             for (int i = 0; i < WI; ++i)
                 __builtin_amdgcn_global_load_lds((gbl_ptr_t)(wsrc[i] + koff),
-                                                 (lds_ptr_t)(st + (wave * WI + i) * 1024), 16, 0, 0);
+                                                 (lds_ptr_t)(st + (wslot * WI + i) * 1024), 16, 0, 0);
         }
+    };
+    auto issue_x = [&](int j) {
+        unsigned char* st = xbuf(j);
+        const int koff = j * (RB / 2);
 #pragma unroll
         for (int i = 0; i < XI; ++i)
-            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(xsrc[i] + koff),
-                                             (lds_ptr_t)(st + WIMG + (wave * XI + i) * 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(xsrc[i] + koff), (lds_ptr_t)(st + (wslot * XI + i) * 1024),
+                                             16, 0, 0);
+    };
+    auto issue = [&](int j) {
+        issue_w(j);
+        issue_x(j);
     };
 
     // ---- fragment addressing: W rows (MFMA A) and x rows (MFMA B); the swizzle term is lane-constant
@@ -158,10 +184,22 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(PPArgs a) {
 #pragma unroll
         for (int t = 0; t < MT; ++t) acc[s][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // ---- prologue: stages 0 .. STAGES-2 in flight
+    // ---- prologue: stages 0 .. STAGES-2 in flight (SPLIT: W chunks 0 .. DW-2 by group 0, x 0 .. DX-2 by group 1)
+    if constexpr (SPLIT) {
+        if (g == 0) {
 #pragma unroll
-    for (int p = 0; p < STAGES - 1; ++p)
-        if (p < NS) issue(p, p);
+            for (int p = 0; p < DW - 1; ++p)
+                if (p < NS) issue_w(p);
+        } else {
+#pragma unroll
+            for (int p = 0; p < DX - 1; ++p)
+                if (p < NS) issue_x(p);
+        }
+    } else {
+#pragma unroll
+        for (int p = 0; p < STAGES - 1; ++p)
+            if (p < NS) issue(p);
+    }
 
     if constexpr (NORMP) {
         // inv[r] of the tile's x rows from the producer's partials, while the first stages are in flight
@@ -174,8 +212,18 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(PPArgs a) {
             if (lane == 0) inv[r] = rsqrtf(ss / (float)K + a.eps);
         }
     }
-    if (NS > STAGES - 2) wait_vmcnt<NPER * (STAGES - 2)>();
-    else wait_vmcnt<0>();
+    if constexpr (SPLIT) {
+        if (g == 0) {
+            if (NS > DW - 2) wait_vmcnt<WI * (DW - 2)>();
+            else wait_vmcnt<0>();
+        } else {
+            if (NS > DX - 2) wait_vmcnt<XI * (DX - 2)>();
+            else wait_vmcnt<0>();
+        }
+    } else {
+        if (NS > STAGES - 2) wait_vmcnt<NPER * (STAGES - 2)>();
+        else wait_vmcnt<0>();
+    }
     pp_bar();
     if (g == 1) pp_bar();  // the stagger: group 1 runs one interval behind group 0
 
@@ -185,13 +233,14 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(PPArgs a) {
 #pragma unroll
     for (int t = 0; t < MT; ++t) fb[t] = bf16x8{};
     const int abl = a.ablate;
-    auto load_frags = [&](const unsigned char* st, int loff) {
+    auto load_frags = [&](int j, int loff) {
         if (abl & 2) return;
+        const unsigned char* wb = wbuf(j);
+        const unsigned char* xb = xbuf(j);
 #pragma unroll
-        for (int s = 0; s < NT; ++s) fa[s] = *reinterpret_cast<const bf16x8*>(st + wrow0[s] * RB + loff);
+        for (int s = 0; s < NT; ++s) fa[s] = *reinterpret_cast<const bf16x8*>(wb + wrow0[s] * RB + loff);
 #pragma unroll
-        for (int t = 0; t < MT; ++t)
-            fb[t] = *reinterpret_cast<const bf16x8*>(st + WIMG + (xrow0 + 16 * t) * RB + loff);
+        for (int t = 0; t < MT; ++t) fb[t] = *reinterpret_cast<const bf16x8*>(xb + (xrow0 + 16 * t) * RB + loff);
     };
     auto mfma_block = [&]() {
         if (abl & 4) return;
@@ -209,37 +258,54 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(PPArgs a) {
         else wait_vmcnt<0>();
     };
 
-    int stg = 0;
-    if constexpr (HALF) {
+    if constexpr (SPLIT) {
+        // group 0: W chunk j+DW-1 in, W chunk j+1 retired after its MFMA block; group 1: x chunk j+DX-1 in, x chunk
+        // j+1 retired after its reads — both before the barrier that ends interval 2j+1
+        for (int j = 0; j < NS; ++j) {
+            if (g == 0) {
+                if (j + DW - 1 < NS && !(abl & 1)) issue_w(j + DW - 1);
+            } else {
+                if (j + DX - 1 < NS && !(abl & 1)) issue_x(j + DX - 1);
+            }
+            load_frags(j, loff0);
+            if (g == 1) {
+                if (j + DX - 1 < NS) wait_vmcnt<XI * (DX - 2)>();
+                else wait_vmcnt<0>();
+            }
+            pp_bar();
+            mfma_block();
+            if (g == 0) {
+                if (j + DW - 1 < NS) wait_vmcnt<WI * (DW - 2)>();
+                else wait_vmcnt<0>();
+            }
+            pp_bar();
+        }
+    } else if constexpr (HALF) {
         // one stage per L/C interval pair; stage j+1 must land before the barrier that ends interval 2j+1
         for (int j = 0; j < NS; ++j) {
-            const unsigned char* st = smem + stg * STAGE;
             const int nx = j + STAGES - 1;
-            if (nx < NS && !(abl & 1)) issue(nx, nx % STAGES);
-            load_frags(st, loff0);
+            if (nx < NS && !(abl & 1)) issue(nx);
+            load_frags(j, loff0);
             if (g == 1) retire_next(nx);
             pp_bar();
             mfma_block();
             if (g == 0) retire_next(nx);
             pp_bar();
-            stg = stg + 1 == STAGES ? 0 : stg + 1;
         }
     } else {
         for (int t = 0; t < NS; ++t) {
-            const unsigned char* st = smem + stg * STAGE;
             const int nx = t + STAGES - 1;
-            if (nx < NS && !(abl & 1)) issue(nx, nx % STAGES);
-            load_frags(st, loff0);  // L0
+            if (nx < NS && !(abl & 1)) issue(nx);
+            load_frags(t, loff0);  // L0
             pp_bar();
             mfma_block();  // C0
             pp_bar();
-            load_frags(st, loff1);  // L1
+            load_frags(t, loff1);  // L1
             if (g == 1) retire_next(nx);
             pp_bar();
             mfma_block();  // C1
             if (g == 0) retire_next(nx);
             pp_bar();
-            stg = stg + 1 == STAGES ? 0 : stg + 1;
         }
     }
     if (g == 0) pp_bar();
@@ -269,14 +335,17 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(PPArgs a) {
         }
         __syncthreads();
         if (!*flag) return;
+        // every slab in slice order, this block's own included: the sum must not depend on which slice arrived last
+        // (bitwise-reproducible outputs, so a captured graph replays exactly what the eager step computed)
         for (int o = 0; o < S; ++o) {
-            if (o == ks) continue;
             const float* sl = a.ws + (int64_t)(tile * S + o) * (BM * BN);
 #pragma unroll
             for (int s = 0; s < NT; ++s)
 #pragma unroll
-                for (int t = 0; t < MT; ++t)
-                    acc[s][t] += *reinterpret_cast<const f32x4*>(sl + (((wave * NT + s) * MT + t) * 64 + lane) * 4);
+                for (int t = 0; t < MT; ++t) {
+                    const f32x4 v = *reinterpret_cast<const f32x4*>(sl + (((wave * NT + s) * MT + t) * 64 + lane) * 4);
+                    acc[s][t] = o == 0 ? v : acc[s][t] + v;
+                }
         }
     }
 
@@ -332,44 +401,48 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(PPArgs a) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i) o[i] = f2bf(acc[s][t][i] * sc);
                     const int n = tn * BN + wrow0[s] + 4 * (lane >> 4);
-                    *reinterpret_cast<u16x4*>(a.y + (int64_t)m * a.N + n) = o;
+                    if (n < a.N) *reinterpret_cast<u16x4*>(a.y + (int64_t)m * a.N + n) = o;  // N % 4 == 0
                 }
             }
         }
     }
 }
 
-template <int BM, int BN, int STAGES, bool HALF, int MODE, bool NORMP, bool PRIO>
+template <int BM, int BN, int STAGES, bool HALF, int MODE, bool NORMP, bool PRIO, int DW, int DX, bool SPLIT>
 void launch_cfg(const PPArgs& a, hipStream_t st) {
-    constexpr int STAGE = (BM + BN) * (HALF ? 64 : 128);
-    const int lds = STAGES * STAGE + 16 + BM * 4;
-    auto kern = gemm_pp_kernel<BM, BN, STAGES, HALF, MODE, NORMP, PRIO>;
+    constexpr int RB = HALF ? 64 : 128;
+    const int lds = (SPLIT ? DW * BN * RB + DX * BM * RB : STAGES * (BM + BN) * RB) + 16 + BM * 4;
+    auto kern = gemm_pp_kernel<BM, BN, STAGES, HALF, MODE, NORMP, PRIO, DW, DX, SPLIT>;
     static bool attr = false;
     if (!attr) {
         hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         attr = true;
     }
     const int mt = (a.M + BM - 1) / BM;
-    const int ntl = MODE == kSwiglu ? a.F / (BN / 2) : a.N / BN;
+    const int ntl = MODE == kSwiglu ? a.F / (BN / 2) : (a.N + BN - 1) / BN;
     hipLaunchKernelGGL(kern, dim3(mt * ntl * a.splitk), dim3(512), lds, st, a);
 }
 
-// tile configs: {BM, BN, STAGES, HALF}
-#define PP_CONFIGS(X)          \
-    X(0, 256, 256, 2, false)   \
-    X(1, 128, 256, 3, false)   \
-    X(2, 256, 128, 3, false)   \
-    X(3, 128, 128, 4, false)   \
-    X(4, 256, 256, 4, true)    \
-    X(5, 128, 256, 6, true)    \
-    X(6, 256, 128, 6, true)    \
-    X(7, 128, 128, 8, true)
+// tile configs: {BM, BN, STAGES, HALF, DW, DX, SPLIT}
+#define PP_CONFIGS(X)                            \
+    X(0, 256, 256, 2, false, 2, 2, false)        \
+    X(1, 128, 256, 3, false, 3, 3, false)        \
+    X(2, 256, 128, 3, false, 3, 3, false)        \
+    X(3, 128, 128, 4, false, 4, 4, false)        \
+    X(4, 256, 256, 4, true, 4, 4, false)         \
+    X(5, 128, 256, 6, true, 6, 6, false)         \
+    X(6, 256, 128, 6, true, 6, 6, false)         \
+    X(7, 128, 128, 8, true, 8, 8, false)         \
+    X(8, 256, 256, 6, true, 6, 3, true)          \
+    X(9, 128, 256, 6, true, 6, 4, true)          \
+    X(10, 256, 128, 8, true, 8, 4, true)         \
+    X(11, 128, 128, 10, true, 10, 6, true)
 
 template <int MODE, bool NORMP, bool PRIO>
 bool launch_mode(int cfg, const PPArgs& a, hipStream_t st) {
     switch (cfg) {
-#define PP_CASE(ID, BM_, BN_, ST_, H_) \
-    case ID: launch_cfg<BM_, BN_, ST_, H_, MODE, NORMP, PRIO>(a, st); return true;
+#define PP_CASE(ID, BM_, BN_, ST_, H_, DW_, DX_, SP_) \
+    case ID: launch_cfg<BM_, BN_, ST_, H_, MODE, NORMP, PRIO, DW_, DX_, SP_>(a, st); return true;
         PP_CONFIGS(PP_CASE)
 #undef PP_CASE
         default: return false;
@@ -380,7 +453,7 @@ bool launch_mode(int cfg, const PPArgs& a, hipStream_t st) {
 
 int gemm_pp_bm(int cfg) {
     switch (cfg) {
-#define PP_BM(ID, BM_, BN_, ST_, H_) case ID: return BM_;
+#define PP_BM(ID, BM_, BN_, ST_, H_, DW_, DX_, SP_) case ID: return BM_;
         PP_CONFIGS(PP_BM)
 #undef PP_BM
         default: return 0;
@@ -388,7 +461,7 @@ int gemm_pp_bm(int cfg) {
 }
 int gemm_pp_bn(int cfg) {
     switch (cfg) {
-#define PP_BN(ID, BM_, BN_, ST_, H_) case ID: return BN_;
+#define PP_BN(ID, BM_, BN_, ST_, H_, DW_, DX_, SP_) case ID: return BN_;
         PP_CONFIGS(PP_BN)
 #undef PP_BN
         default: return 0;

@@ -477,6 +477,9 @@ class StepBatch:
     # context-parallel prefill (parallel/context_parallel.py): this rank holds part of a long chunk; K/V are
     # all-gathered per layer and written for every token of the chunk
     cp: Optional[object] = None
+    # mixed step: decode rows (a decode-mode StepBatch over device slot state) appended after this batch's prefill
+    # tokens — one forward, shared projections; ``last_idx`` then also lists the decode rows (after the prefill rows)
+    dec: Optional["StepBatch"] = None
 
 
 def make_prefill_batch(prompts: list[list[int]], starts: list[int], block_tables: list[list[int]], cfg: LlamaConfig,
@@ -533,7 +536,7 @@ def h2d(t: torch.Tensor | None, device) -> torch.Tensor | None:
 def to_device(sb: StepBatch, device) -> StepBatch:
     mv = lambda t: h2d(t, device)  # noqa: E731
     return StepBatch(mv(sb.ids), mv(sb.pos), mv(sb.tok_seq), mv(sb.block_table), mv(sb.q_start), mv(sb.ctx_len),
-                     mv(sb.last_idx), mv(sb.tiles), sb.ntiles, sb.nqt, sb.nsplit, sb.parts)
+                     mv(sb.last_idx), mv(sb.tiles), sb.ntiles, sb.nqt, sb.nsplit, sb.parts, sb.cp, sb.dec)
 
 
 # -----------------------------------------------------------------------------------------------------------------
@@ -571,45 +574,63 @@ class LlamaModel:
         return ops.rmsnorm(h, w, eps) if resid is None else ops.add_rmsnorm(h, resid, w, eps)
 
     def _out_proj(self, x: torch.Tensor, w: torch.Tensor, st: dict):
-        """Row-parallel output projection (o_proj / down_proj).  TP=1 decode (T <= 2): the GEMV that also adds the
-        residual and emits the next RMSNorm's partial sums (ops.ResidOut) — the norm then costs no launch."""
+        """Row-parallel output projection (o_proj / down_proj).  TP=1: the producer that also adds the residual and
+        emits the next RMSNorm's partial sums (ops.ResidOut: the decode GEMV at T <= 2, the batched GEMM's kResid
+        epilogue above, prefill included) — the norm then costs no launch: its consumer (QKV / gate_up / LM head)
+        applies it as a per-row scale."""
         T = st["T"]
-        if (_FUSE_NORM and self.w.norms_folded and self.tp.world == 1 and x.is_cuda and st["sb"].tiles is None
-                and ops.resid_ok(T, w.shape[0], w.shape[1])):
+        if (_FUSE_NORM and self.w.norms_folded and self.tp.world == 1 and x.is_cuda and st["sb"].cp is None
+                and (st["sb"].tiles is None or T > 2) and ops.resid_ok(T, w.shape[0], w.shape[1])):
             return ops.gemv_resid(x, w, st["resid"])
         return ops.linear(x, w)
 
-    def _attn(self, li: int, lw: LayerWeights, st: dict, kv: KVCache) -> torch.Tensor:
-        """Attention block up to the row-parallel o_proj; returns this rank's partial sum."""
-        sb, T, x = st["sb"], st["T"], st["x"]
+    def _attn_rows(self, li: int, qkv: torch.Tensor, sb: StepBatch, q_buf: torch.Tensor, kv: KVCache) -> torch.Tensor:
+        """RoPE + paged-KV write + attention for the rows of one step batch (prefill tiles or decode rows)."""
+        T = qkv.shape[0]
         attn = None
-        if (not self.w.fp8 and _FUSE_NORM and ops.qkv_rope(
+        if _FUSE_DECODE_ROPE and sb.tiles is None and sb.cp is None and sb.nqt == 1 and sb.nsplit == 1:
+            # batched decode: RoPE + KV write inside the one-wave decode attention (None off its shapes)
+            attn = ops.decode_attention_rope(qkv, sb.pos, self.cos_sin, kv.k[li], kv.v[li], sb.block_table,
+                                             sb.ctx_len, T, self.hq, self.scale)
+        if attn is None:
+            ops.rope_kv_write(qkv, sb.pos, sb.tok_seq, sb.block_table, self.cos_sin, q_buf, kv.k[li], kv.v[li],
+                              self.hq, self.hkv, True, kv.k_scale[li], kv.v_scale[li])
+        if sb.cp is not None:  # CP: every rank writes the whole chunk's K/V before any rank attends
+            from ..parallel.context_parallel import gather_kv
+
+            cp = sb.cp
+            ops.rope_kv_write(gather_kv(qkv, self.hq, cp), cp.pos_all, cp.seq_all, cp.bt, self.cos_sin,
+                              cp.dummy_q, kv.k[li], kv.v[li], 0, self.hkv, False, kv.k_scale[li], kv.v_scale[li])
+        if attn is None:
+            attn = ops.paged_attention(q_buf, kv.k[li], kv.v[li], sb.block_table, sb.q_start, sb.ctx_len, sb.tiles,
+                                       sb.ntiles, sb.nqt, sb.nsplit, self.scale, kv.k_scale[li], kv.v_scale[li])
+        return attn.view(T, -1)
+
+    def _attn(self, li: int, lw: LayerWeights, st: dict, kv: KVCache) -> torch.Tensor:
+        """Attention block up to the row-parallel o_proj; returns this rank's partial sum.  A mixed step (``sb.dec``)
+        runs the projections over prefill and decode rows together and the attention of each part with its own
+        kernel (flash / split-K prefill tiles; the decode kernel for the one-token rows)."""
+        sb, T, x = st["sb"], st["T"], st["x"]
+        if (sb.dec is None and not self.w.fp8 and _FUSE_NORM and ops.qkv_rope(
                 x, lw.wqkv, sb.pos, sb.tok_seq, sb.block_table, self.cos_sin, st["q_buf"], kv.k[li], kv.v[li],
                 self.hq, self.hkv, kv.k_scale[li], kv.v_scale[li])):
-            pass  # decode: QKV GEMV (+ folded norm) + RoPE / paged-KV write in one launch
-        else:
-            x = ops.LazyNorm.force(x)
-            qkv = ops.qlinear(*x, lw.wqkv.q, lw.wqkv.s) if self.w.fp8 else ops.linear(x, lw.wqkv)
-            if _FUSE_DECODE_ROPE and sb.tiles is None and sb.cp is None and sb.nqt == 1 and sb.nsplit == 1:
-                # batched decode: RoPE + KV write inside the one-wave decode attention (None off its shapes)
-                attn = ops.decode_attention_rope(qkv, sb.pos, self.cos_sin, kv.k[li], kv.v[li], sb.block_table,
-                                                 sb.ctx_len, T, self.hq, self.scale)
-            if attn is None:
-                ops.rope_kv_write(qkv, sb.pos, sb.tok_seq, sb.block_table, self.cos_sin, st["q_buf"], kv.k[li],
-                                  kv.v[li], self.hq, self.hkv, True, kv.k_scale[li], kv.v_scale[li])
-            if sb.cp is not None:  # CP: every rank writes the whole chunk's K/V before any rank attends
-                from ..parallel.context_parallel import gather_kv
-
-                cp = sb.cp
-                ops.rope_kv_write(gather_kv(qkv, self.hq, cp), cp.pos_all, cp.seq_all, cp.bt, self.cos_sin,
-                                  cp.dummy_q, kv.k[li], kv.v[li], 0, self.hkv, False, kv.k_scale[li], kv.v_scale[li])
-        if attn is None:
+            # decode: QKV GEMV (+ folded norm) + RoPE / paged-KV write in one launch
             attn = ops.paged_attention(st["q_buf"], kv.k[li], kv.v[li], sb.block_table, sb.q_start, sb.ctx_len,
                                        sb.tiles, sb.ntiles, sb.nqt, sb.nsplit, self.scale, kv.k_scale[li],
-                                       kv.v_scale[li])
+                                       kv.v_scale[li]).view(T, -1)
+        else:
+            # a LazyNorm input goes straight to the projection (the batched GEMM applies the folded norm as a row
+            # scale; anything else materialises it)
+            qkv = ops.qlinear(*x, lw.wqkv.q, lw.wqkv.s) if self.w.fp8 else ops.linear(x, lw.wqkv)
+            if sb.dec is None:
+                attn = self._attn_rows(li, qkv, sb, st["q_buf"], kv)
+            else:
+                tp_ = T - sb.dec.ntiles
+                attn = torch.cat([self._attn_rows(li, qkv[:tp_], sb, st["q_buf"][:tp_], kv),
+                                  self._attn_rows(li, qkv[tp_:], sb.dec, st["q_buf"][tp_:], kv)])
         if self.w.fp8:
-            return ops.qlinear(*ops.quant_rows(attn.view(T, -1)), lw.wo.q, lw.wo.s)
-        return self._out_proj(attn.view(T, -1), lw.wo, st)
+            return ops.qlinear(*ops.quant_rows(attn), lw.wo.q, lw.wo.s)
+        return self._out_proj(attn, lw.wo, st)
 
     def _mlp(self, lw: LayerWeights, st: dict) -> torch.Tensor:
         """SwiGLU MLP up to the row-parallel down_proj; returns this rank's partial sum."""
@@ -654,7 +675,8 @@ class LlamaModel:
         Single part (decode, TP=1): the same ops in the same order with synchronous all-reduces (graph-capturable, the
         IPC one-shot kernel for decode-sized messages)."""
         cfg, w, tp = self.cfg, self.w, self.tp
-        if tp.world > 1 and sb.tiles is not None and self.sequence_parallel and not w.fp8 and sb.cp is None:
+        if (tp.world > 1 and sb.tiles is not None and self.sequence_parallel and not w.fp8 and sb.cp is None
+                and sb.dec is None):
             return self._forward_sp(sb, kv, logits_dtype)
         parts = sb.parts if (sb.parts and tp.world > 1) else [sb]
         overlap = len(parts) > 1
@@ -669,8 +691,9 @@ class LlamaModel:
             ar = lambda t: (tp.all_reduce(t), None)  # noqa: E731
         states = []
         for p in parts:
-            h = tp.all_reduce(ops.embedding(p.ids, w.embed, w.vocab_start))
-            T = p.ids.numel()
+            ids = p.ids if p.dec is None else torch.cat([p.ids, p.dec.ids])
+            h = tp.all_reduce(ops.embedding(ids, w.embed, w.vocab_start))
+            T = ids.numel()
             st = dict(sb=p, T=T, resid=h, q_buf=torch.empty(T, self.hq, cfg.head_dim, device=h.device, dtype=h.dtype))
             st["x"] = self._norm(h, st, w.layers[0].attn_norm, first=True)
             states.append(st)
@@ -692,6 +715,10 @@ class LlamaModel:
                     st["x"] = self._norm(dn, st, w.norm)
                 elif fuse and st["sb"].tiles is None:  # TP decode: every token is sampled
                     st["x"] = self._norm(dn, st, w.norm, reduce=True)
+                elif isinstance(dn, ops.ResidOut):  # prefill producer: the sampled rows' stream and partials
+                    li_ = st["sb"].last_idx
+                    st["x"] = ops.LazyNorm(dn.s.index_select(0, li_), dn.part.index_select(0, li_), w.norm,
+                                           cfg.rms_eps)
                 else:  # only the sampled rows need the final norm + LM head (bf16)
                     if fuse:
                         dn = tp.all_reduce(dn)

@@ -1,18 +1,17 @@
 """Projection GEMMs.
 
 ``linear(x, w)`` computes ``x @ w.T`` for weights stored [out, in] (HF layout); ``gate_up_silu`` is the fused K8+K9.
-Routing is by measured shape (profiles/r1_gemm_vs_hipblaslt.json, cold weights, one MI355X):
+Routing is by measured shape:
 
 * M <= 2 (single-stream decode): the hand-written GEMV (csrc/kernels/gemv.hip), 1 KiB row-contiguous weight
   streaming — beats hipBLASLt on every decode shape;
-* gate_up at 3 <= M <= 128: the MFMA GEMM with the fused SwiGLU epilogue (csrc/kernels/gemm.hip) — 1.05-1.24x over
-  hipBLASLt + the separate silu_mul pass, which it removes;
-* everything else: hipBLASLt via torch.matmul (the "plain library GEMM" rule).  Measured alternatives that did not
-  pay at the wave's M = 1024 decode bucket: a TunableOp sweep over every library solution (~1 % of the wave,
-  profiles/r1s4_tunableop_gemm_study.jsonl) and two half-batches on two HIP streams so the under-filled N = 4096 /
-  6144 projections run side by side (-2 % decode GPU time, but a slower wave: 580 vs 608 chains/s).  The hand-written 128x128-tile MFMA
-  GEMM loses there: one tile per CU is bound by the per-CU load path (~0.7 us per 64-deep K-step), the same wall
-  hipBLASLt's 128x128 tiles hit, and it has no answer to the small-grid shapes (N = 4096 at M <= 128).
+* M >= 3: the hand-written ping-pong MFMA GEMM family (csrc/kernels/gemm_pp.hip) with its fused epilogues — the
+  decoder's residual add + RMSNorm partial sums on O / down (``pp_resid`` -> ResidOut), the folded RMSNorm as a
+  per-row scale on QKV / gate_up / LM head (a LazyNorm input), SwiGLU on gate_up — with the tile config and split-K
+  of the measured plan (``gemm_plan.json``: per (N, K, epilogue) the best of the configs by M range, from
+  ``scripts/bench_gemm_pp.py`` on one MI355X, random operands, cold weights);
+* hipBLASLt (torch.matmul) only where the plan records that the library wins by more than 3 % (the "plain library
+  GEMM" rule), or for shapes the kernel does not take (K % 64, N % 4).  CHRONOS_PP=lib|own|auto forces a side.
 """
 from __future__ import annotations
 
@@ -24,6 +23,91 @@ import torch
 
 # Largest M routed to the GEMV (gemv_ok).  Env CHRONOS_GEMV_MAX_M; scripts/single_stream.py A/Bs it (py_gemv_max_m).
 GEMV_MAX_M = int(os.environ.get("CHRONOS_GEMV_MAX_M", "2"))
+
+# ---- the batched GEMM family (gemm_pp.hip) ----------------------------------------------------------------------
+PP_MODE = os.environ.get("CHRONOS_PP", "auto")  # auto | own | lib
+PP_PLAIN, PP_SWIGLU, PP_RESID = 0, 1, 2
+_PP_BM = {0: 256, 1: 128, 2: 256, 3: 128, 4: 256, 5: 128, 6: 256, 7: 128, 8: 256, 9: 128, 10: 256, 11: 128}
+_PP_BN = {0: 256, 1: 256, 2: 128, 3: 128, 4: 256, 5: 256, 6: 128, 7: 128, 8: 256, 9: 256, 10: 128, 11: 128}
+# relative per-CU MAC rate of each tile config at full occupancy (gate_up M = 1024 sweep, profiles/r3_gemm_pp_*)
+_PP_RATE = {0: 1.0, 1: 0.84, 2: 0.84, 3: 0.66, 4: 1.0, 5: 0.71, 6: 0.73, 7: 0.6, 8: 1.0, 9: 0.84, 10: 0.84, 11: 0.66}
+_plan_cache: dict = {}
+_plan_table: Optional[dict] = None
+
+
+def _plan_file() -> dict:
+    global _plan_table
+    if _plan_table is None:
+        import json
+
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_plan.json")
+        try:
+            with open(path) as fh:
+                raw = json.load(fh)
+            _plan_table = {tuple(int(v) for v in key.split(",")): rows for key, rows in raw.get("plans", {}).items()}
+        except FileNotFoundError:
+            _plan_table = {}
+    return _plan_table
+
+
+def _pp_valid(cfg: int, n: int, k: int, mode: int, sk: int) -> bool:
+    bn = _PP_BN[cfg]
+    if k % 64 or (k // 64) % sk:
+        return False
+    return n % 4 == 0 if mode == PP_PLAIN else n % bn == 0
+
+
+def _pp_model(m: int, n: int, k: int, mode: int, cus: int = 256) -> tuple[int, int]:
+    """Cost-model pick for a shape the measured plan does not list: whole rounds of tiles over the CUs at each
+    config's per-CU rate, plus the split-K slab traffic."""
+    best, arg = None, (0, 1)
+    for cfg in (0, 1, 2, 3):
+        bm, bn = _PP_BM[cfg], _PP_BN[cfg]
+        tiles = -(-m // bm) * -(-n // bn)
+        for sk in (1, 2, 4):
+            if not _pp_valid(cfg, n, k, mode, sk) or (sk > 1 and tiles * sk > 2 * cus):
+                continue
+            rounds = -(-tiles * sk // cus)
+            t = rounds * bm * bn * (k // sk) / _PP_RATE[cfg] / 256.0 ** 2 + (sk > 1) * tiles * sk * bm * bn * 4 / 5e5
+            if best is None or t < best:
+                best, arg = t, (cfg, sk)
+    return arg
+
+
+def pp_plan(m: int, n: int, k: int, mode: int = PP_PLAIN) -> Optional[tuple[int, int]]:
+    """(tile config, split-K) of the hand-written batched GEMM for this shape, or None for the library."""
+    if m < 3 or PP_MODE == "lib":
+        return None
+    key = (m, n, k, mode)
+    hit = _plan_cache.get(key, False)
+    if hit is not False:
+        return hit
+    out = None
+    if k % 64 == 0 and (n % 4 == 0 if mode == PP_PLAIN else n % 128 == 0):
+        rows = _plan_file().get((n, k, mode))
+        if rows and PP_MODE != "own":
+            for m_hi, cfg, sk in rows:  # sorted by m_hi; cfg < 0 = the library measured faster
+                if m <= m_hi:
+                    out = None if cfg < 0 else (cfg, sk)
+                    break
+            else:
+                out = _pp_model(m, n, k, mode)
+        else:
+            out = _pp_model(m, n, k, mode)
+        if out is not None and not _pp_valid(out[0], n, k, mode, out[1]):
+            out = None
+    _plan_cache[key] = out
+    return out
+
+
+def pp_gemm(x: torch.Tensor, w: torch.Tensor, mode: int, plan: tuple[int, int], resid=None, part=None,
+            eps: float = 1e-5):
+    """One launch of gemm_pp.hip: returns (y, partials) — partials only for the residual epilogue."""
+    from . import _k
+
+    k = x.shape[-1]
+    y, pt = _k().gemm_pp(x.reshape(-1, k), w, mode, plan[0], plan[1], resid, part, eps, False)
+    return y, pt
 
 # (M, N, K) -> bool predicate + kernel; extension point for further shape-specialised kernels
 _custom: list[tuple[Callable[[int, int, int], bool], Callable[[torch.Tensor, torch.Tensor], torch.Tensor]]] = []
@@ -79,17 +163,25 @@ class LazyNorm:
 
 
 def gemv_resid(x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor) -> ResidOut:
-    """Decode producer: the new residual stream and the RMSNorm partials in one GEMV launch (M <= 2)."""
+    """Producer (O / down projection, TP=1): the new residual stream s = bf16(bf16(x @ w.T) + resid) and the RMSNorm
+    partial sums of s^2, in one launch — the GEMV at M <= 2, the batched GEMM's kResid epilogue above."""
     from . import _k
 
+    m, k = x.numel() // x.shape[-1], x.shape[-1]
+    if m > 2:
+        s, part = pp_gemm(x, w, PP_RESID, pp_plan(m, w.shape[0], k, PP_RESID), resid.reshape(m, -1))
+        return ResidOut(s.view(resid.shape), part)
     s = torch.empty(resid.shape, dtype=resid.dtype, device=resid.device)
     part = _k().gemv_resid(x.reshape(-1, x.shape[-1]), w, resid, s)
     return ResidOut(s, part)
 
 
 def resid_ok(m: int, n: int, k: int) -> bool:
-    """Shapes of the residual-epilogue producer (gemv.hip kResid): the M <= 2 GEMV shapes."""
-    return m <= 2 and gemv_ok(m, n, k)
+    """Shapes of the residual-epilogue producer: the M <= 2 GEMV shapes (gemv.hip kResid) and the batched GEMM's
+    (gemm_pp.hip kResid) where the plan takes it."""
+    if m <= 2:
+        return gemv_ok(m, n, k)
+    return pp_plan(m, n, k, PP_RESID) is not None
 
 
 def gemv_ok(m: int, n: int, k: int, swiglu: bool = False) -> bool:
@@ -122,18 +214,27 @@ def mfma_gemm(x: torch.Tensor, w: torch.Tensor, swiglu: bool = False, stages: in
 
 
 def gate_up_silu(x: torch.Tensor, w_gu: torch.Tensor) -> torch.Tensor:
-    """silu(x @ gate.T) * (x @ up.T) with w_gu = [gate; up]: one fused launch for decode batches, else GEMM + silu_mul."""
+    """silu(x @ gate.T) * (x @ up.T) with w_gu = [gate; up]: one fused launch (GEMV at M <= 2, the batched GEMM's
+    SwiGLU epilogue above, with the folded input norm when x is a LazyNorm), else GEMM + silu_mul."""
     from . import _k, silu_mul
 
     if isinstance(x, LazyNorm):
         m, n, k = x.rows(), w_gu.shape[0], x.shape[-1]
         if x.fusable() and gemv_ok(m, n, k, swiglu=True):
             return _k().gemv_normp(x.s, x.part, x.eps, w_gu, True)
+        plan = pp_plan(m, n, k, PP_SWIGLU) if x.fusable() else None
+        if plan is not None:
+            y, _ = pp_gemm(x.s, w_gu, PP_SWIGLU, plan, None, x.part, x.eps)
+            return y.view(*x.shape[:-1], n // 2)
         x = x.materialize()
     if x.is_cuda:
         m, n, k = x.numel() // x.shape[-1], w_gu.shape[0], x.shape[-1]
         if gemv_ok(m, n, k, swiglu=True):
             return _gemv(x, w_gu, True)
+        plan = pp_plan(m, n, k, PP_SWIGLU)
+        if plan is not None:
+            y, _ = pp_gemm(x, w_gu, PP_SWIGLU, plan)
+            return y.view(*x.shape[:-1], n // 2)
         if mfma_swiglu_ok(m, n, k):
             return mfma_gemm(x, w_gu, True)
     return silu_mul(linear(x, w_gu))
@@ -141,10 +242,15 @@ def gate_up_silu(x: torch.Tensor, w_gu: torch.Tensor) -> torch.Tensor:
 
 def linear(x, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     if isinstance(x, LazyNorm):
-        if x.fusable() and out is None and gemv_ok(x.rows(), w.shape[0], x.shape[-1]):
+        m, n, k = x.rows(), w.shape[0], x.shape[-1]
+        if x.fusable() and out is None and gemv_ok(m, n, k):
             from . import _k
 
             return _k().gemv_normp(x.s, x.part, x.eps, w, False)
+        plan = pp_plan(m, n, k, PP_PLAIN) if x.fusable() and out is None else None
+        if plan is not None:
+            y, _ = pp_gemm(x.s, w, PP_PLAIN, plan, None, x.part, x.eps)
+            return y.view(*x.shape[:-1], n)
         x = x.materialize()
     if x.is_cuda:
         m, k = x.numel() // x.shape[-1], x.shape[-1]
@@ -154,6 +260,10 @@ def linear(x, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tens
         for pred, fn in _custom:
             if pred(m, n, k):
                 return fn(x, w)
+        plan = pp_plan(m, n, k, PP_PLAIN) if out is None else None
+        if plan is not None:
+            y, _ = pp_gemm(x, w, PP_PLAIN, plan)
+            return y.view(*x.shape[:-1], n)
     if out is not None:
         return torch.matmul(x, w.t(), out=out)
     return torch.matmul(x, w.t())

@@ -22,8 +22,8 @@ SHAPES = {  # name: (N, K, mode)  mode 1 = swiglu (N = 2F)
     "down": (4096, 14336, 2),
     "lm_head": (128256, 4096, 0),
 }
-BM = {0: 256, 1: 128, 2: 256, 3: 128, 4: 256, 5: 128, 6: 256, 7: 128}
-BN = {0: 256, 1: 256, 2: 128, 3: 128, 4: 256, 5: 256, 6: 128, 7: 128}
+BM = {0: 256, 1: 128, 2: 256, 3: 128, 4: 256, 5: 128, 6: 256, 7: 128, 8: 256, 9: 128, 10: 256, 11: 128}
+BN = {0: 256, 1: 256, 2: 128, 3: 128, 4: 256, 5: 256, 6: 128, 7: 128, 8: 256, 9: 256, 10: 128, 11: 128}
 
 
 def candidates(m, n, k, mode, cus=256):

@@ -1,0 +1,139 @@
+"""Measure the batched GEMM family (gemm_pp.hip) against hipBLASLt on every projection shape of the served models and
+write the routing plan ops/gemm_plan.json (+ a per-shape table for profiles/).
+
+For each (N, K, epilogue) and each M bucket: the fastest tile config / split-K among the cost model's candidates,
+timed interleaved with the library path of the same epilogue (library GEMM + silu_mul for SwiGLU, + the residual add
+for the residual epilogue) in one process on cold weights (cdna_hip_programming.md §5.4 rule 24).  The plan keeps
+the hand-written kernel unless the library is more than 3 % faster (any shape left on the library needs a
+recorded A/B where the hand-written kernel loses by > 3 %).
+
+  python scripts/tune_gemm_pp.py [--models 8b,70b-tp8] [--ms 3,8,...] [--out-plan P] [--out-table T]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+SHAPES = {
+    "8b": {"qkv": (6144, 4096, 0), "o": (4096, 4096, 2), "gate_up": (28672, 4096, 1), "down": (4096, 14336, 2),
+           "lm_head": (128256, 4096, 0)},
+    # Llama-3-70B, TP=8 shards (column-parallel QKV / gate_up / LM head, row-parallel O / down: plain epilogue, the
+    # residual add follows the all-reduce)
+    "70b-tp8": {"qkv": (1280, 8192, 0), "o": (8192, 1024, 0), "gate_up": (7168, 8192, 1), "down": (8192, 3584, 0),
+                "lm_head": (16032, 8192, 0)},
+}
+MS = [3, 8, 16, 32, 64, 128, 256, 512, 768, 1024, 2048, 4096, 8192, 16384]
+
+
+def candidates(m, n, k, mode, keep=6):
+    from chronos.ops import gemm as G
+
+    scored = []
+    for cfg in G._PP_BM:
+        bm, bn = G._PP_BM[cfg], G._PP_BN[cfg]
+        tiles = -(-m // bm) * -(-n // bn)
+        for sk in (1, 2, 4, 8):
+            if not G._pp_valid(cfg, n, k, mode, sk) or (sk > 1 and (tiles >= 256 or tiles * sk > 512)):
+                continue
+            if m >= 4096 and sk > 1:
+                continue
+            rounds = -(-tiles * sk // 256)
+            t = rounds * bm * bn * (k // sk) / G._PP_RATE[cfg] + (sk > 1) * tiles * sk * bm * bn * 4 * 2e3
+            scored.append((t, cfg, sk))
+    scored.sort()
+    out = [(c, s) for _, c, s in scored[:keep]]
+    for must in ((0, 1), (4, 1), (8, 1)):
+        if must not in out and G._pp_valid(must[0], n, k, mode, 1):
+            out.append(must)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--models", default="8b,70b-tp8")
+    ap.add_argument("--ms", default=",".join(str(m) for m in MS))
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--iters", type=int, default=8)
+    ap.add_argument("--out-plan", default="")
+    ap.add_argument("--out-table", default="")
+    args = ap.parse_args()
+    from chronos import ops
+
+    ops.load()
+    dev = "cuda"
+    ms = [int(v) for v in args.ms.split(",")]
+    plans, table = {}, []
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for model in args.models.split(","):
+        for op, (n, k, mode) in SHAPES[model].items():
+            g = torch.Generator(device=dev).manual_seed(0)
+            ncopy = max(2, -(-(600 << 20) // (n * k * 2)))
+            ws = [((torch.rand(n, k, device=dev, generator=g) * 2 - 1) * 0.05).to(torch.bfloat16)
+                  for _ in range(ncopy)]
+            rows = []
+            for m in ms:
+                if op == "lm_head" and m > 2048:  # the LM head only sees the sampled rows (<= the decode batch)
+                    continue
+                x = (torch.rand(m, k, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
+                resid = (torch.rand(m, n, device=dev, generator=g) * 2 - 1).to(torch.bfloat16) if mode == 2 else None
+
+                def lib(i):
+                    y = x @ ws[i % ncopy].t()
+                    return ops.silu_mul(y) if mode == 1 else (y + resid if mode == 2 else y)
+
+                def own(i, c):
+                    return torch.ops.chronos.gemm_pp(x, ws[i % ncopy], mode, c[0], c[1], resid, None, 1e-5, False)[0]
+
+                cands = candidates(m, n, k, mode)
+                ref = lib(0).float()
+                scale = ref.abs().max().item() + 1e-6
+                bad = [c for c in cands if (own(0, c).float() - ref).abs().max().item() > 0.03 * scale]
+                assert not bad, f"{op} M={m}: wrong results from {bad}"
+                times = {c: [] for c in ["lib"] + cands}
+                flop = 2.0 * m * n * k
+                iters = max(2, min(args.iters, int(2e13 / flop) + 2))
+                for _ in range(args.rounds):
+                    for c in times:
+                        fn = (lambda i: lib(i)) if c == "lib" else (lambda i, c=c: own(i, c))
+                        fn(0)
+                        torch.cuda.synchronize()
+                        st.record()
+                        for i in range(iters):
+                            fn(i)
+                        en.record()
+                        torch.cuda.synchronize()
+                        times[c].append(st.elapsed_time(en) * 1000 / iters)
+                best = min(cands, key=lambda c: min(times[c]))
+                lib_us, own_us = min(times["lib"]), min(times[best])
+                use_lib = lib_us < own_us / 1.03
+                rows.append([m, -1 if use_lib else best[0], 1 if use_lib else best[1]])
+                rec = dict(model=model, op=op, m=m, n=n, k=k, mode=mode, lib_us=round(lib_us, 2),
+                           own_us=round(own_us, 2), own=f"cfg{best[0]}_sk{best[1]}",
+                           lib_TF=round(flop / lib_us / 1e6, 1), own_TF=round(flop / own_us / 1e6, 1),
+                           speedup=round(lib_us / own_us, 3), route="lib" if use_lib else "own",
+                           all={f"cfg{c[0]}_sk{c[1]}": round(min(times[c]), 2) for c in cands})
+                table.append(rec)
+                print(json.dumps(rec), flush=True)
+            # plan rows: a measured M decides (previous measured M, M] (its tiles cover any M up to it); the last
+            # one also everything above
+            keyed = [[m if i + 1 < len(rows) else 1 << 30, cfg, sk] for i, (m, cfg, sk) in enumerate(rows)]
+            plans[f"{n},{k},{mode}"] = keyed
+            del ws
+            torch.cuda.empty_cache()
+    meta = {"device": torch.cuda.get_device_name(0), "note": "rows: [M upper bound, cfg (-1 = library), split-K]"}
+    if args.out_plan:
+        with open(args.out_plan, "w") as fh:
+            json.dump({"meta": meta, "plans": plans}, fh, indent=1)
+    if args.out_table:
+        with open(args.out_table, "w") as fh:
+            fh.writelines(json.dumps(r) + "\n" for r in table)
+    won = sum(r["route"] == "own" for r in table)
+    print(f"hand-written kernel routed on {won}/{len(table)} (shape, M) points", flush=True)
+
+
+if __name__ == "__main__":
+    main()

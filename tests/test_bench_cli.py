@@ -44,3 +44,29 @@ def test_bench_two_ranks(tp, sp):
     else:
         assert r["config"]["parallelism"] == "tp2" and r["config"]["global_batch"] == 3
         assert r["verdicts_valid"] == "3/3" and "TP=2" in r["metric"]
+
+
+def _run_plain(gpus_args, env_extra=None, timeout=600):
+    cmd = [sys.executable, os.path.join(REPO, "bench.py")] + gpus_args + [
+        "--device", "cpu", "--model", "tiny", "--streams", "3", "--steps", "1", "--warmup", "1",
+        "--num-predict", "24", "--single-stream", "2", "--no-graphs", "--max-model-len", "384"]
+    env = dict(os.environ, OMP_NUM_THREADS="2", **(env_extra or {}))
+    env.pop("WORLD_SIZE", None) if not env_extra or "WORLD_SIZE" not in env_extra else None
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env, cwd=REPO)
+
+
+@pytest.mark.slow
+def test_bench_gpus_flag_self_launches():
+    """`python bench.py --gpus 2` with no launcher runs 2 ranks (--gpus was ignored) and reports both
+    replicas' chains."""
+    out = _run_plain(["--gpus", "2"])
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 2 and r["config"]["parallelism"] == "dp2" and r["verdicts_valid"] == "6/6"
+
+
+def test_bench_gpus_mismatch_is_an_error():
+    out = _run_plain(["--gpus", "2"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"}, timeout=300)
+    assert out.returncode != 0 and "disagrees with WORLD_SIZE" in out.stderr

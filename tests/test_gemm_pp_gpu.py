@@ -35,7 +35,7 @@ def _check(y, ref, tol=2e-2):
     assert err <= tol * scale, f"max err {err:.4g} vs max |ref| {scale:.4g}"
 
 
-CFGS = [0, 1, 2, 3, 4, 5, 6, 7]
+CFGS = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11]
 
 
 @pytest.mark.parametrize("cfg", CFGS)
@@ -49,7 +49,18 @@ def test_plain(cfg, m):
     _check(y, x.float() @ w.float().t())
 
 
-@pytest.mark.parametrize("cfg,splitk", [(0, 2), (1, 4), (3, 2), (2, 5), (4, 2), (5, 4), (7, 2)])
+@pytest.mark.parametrize("cfg", [0, 3, 5, 8, 11])
+def test_n_tail(cfg):
+    """N not a multiple of the tile (the 70B TP=8 LM-head shard is N = 16032): the last W tile is partial."""
+    g = torch.Generator(device=DEV).manual_seed(21 + cfg)
+    m, n, k = 77, 16032 // 8, 256
+    x = _rand((m, k), g)
+    w = _rand((n, k), g, 0.5)
+    y, _ = _pp(x, w, 0, cfg, 2)
+    _check(y, x.float() @ w.float().t())
+
+
+@pytest.mark.parametrize("cfg,splitk", [(0, 2), (1, 4), (3, 2), (2, 5), (4, 2), (5, 4), (7, 2), (8, 2), (9, 4), (10, 2), (11, 5)])
 def test_splitk(cfg, splitk):
     g = torch.Generator(device=DEV).manual_seed(11 + cfg)
     m, n, k = 300, 512, 64 * 20
@@ -61,7 +72,7 @@ def test_splitk(cfg, splitk):
         _check(y, ref)
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 3, 4, 5])
+@pytest.mark.parametrize("cfg", [0, 1, 3, 4, 5, 8, 9, 11])
 def test_swiglu_normp(cfg):
     g = torch.Generator(device=DEV).manual_seed(3 + cfg)
     m, f, k = 200, 256, 512
@@ -80,7 +91,7 @@ def test_swiglu_normp(cfg):
     _check(y2, hv)
 
 
-@pytest.mark.parametrize("cfg,splitk", [(0, 1), (1, 2), (3, 1), (4, 1), (5, 2)])
+@pytest.mark.parametrize("cfg,splitk", [(0, 1), (1, 2), (3, 1), (4, 1), (5, 2), (8, 1), (9, 2), (10, 1)])
 def test_resid_partials(cfg, splitk):
     g = torch.Generator(device=DEV).manual_seed(5 + cfg)
     m, n, k = 259, 512, 768

@@ -75,9 +75,10 @@ def test_engine_partial_prefix_same_outputs(partial):
     chains = synthetic_chains(12, seed=11, native=False)
     outs, stats = [], []
     for pc in (False, True):
+        # non-mixed scheduling: both runs batch every decode row identically, so outputs must match bit for bit
         eng = Engine(EngineConfig(model="tiny", device="cpu", max_slots=16, max_model_len=384, use_graphs=False,
                                   prefix_cache=pc, partial_prefix=partial, max_prefill_tokens=120, prefill_ramp=0,
-                                  jump_forward=False))
+                                  jump_forward=False, mixed_batching=False))
         reqs = [eng.submit(build_prompt(c.history), fmt=VERDICT_SCHEMA, num_predict=20) for c in chains]
         eng.run_until_idle()
         outs.append([r.out_ids for r in reqs])
@@ -97,7 +98,7 @@ def test_engine_prefix_cache_same_outputs(chunk):
     outs, stats = [], []
     for pc in (False, True):
         eng = Engine(EngineConfig(model="tiny", device="cpu", max_slots=8, max_model_len=384, use_graphs=False,
-                                  prefix_cache=pc, max_prefill_tokens=chunk))
+                                  prefix_cache=pc, max_prefill_tokens=chunk, mixed_batching=False))
         reqs = [eng.submit(build_prompt(c.history), fmt=VERDICT_SCHEMA, num_predict=30) for c in chains]
         eng.run_until_idle()
         outs.append([r.out_ids for r in reqs])
