@@ -85,15 +85,14 @@ def pp_plan(m: int, n: int, k: int, mode: int = PP_PLAIN) -> Optional[tuple[int,
     out = None
     if k % 64 == 0 and (n % 4 == 0 if mode == PP_PLAIN else n % 128 == 0):
         rows = _plan_file().get((n, k, mode))
-        if rows and PP_MODE != "own":
+        if PP_MODE == "own":
+            out = _pp_model(m, n, k, mode)
+        elif rows:
             for m_hi, cfg, sk in rows:  # sorted by m_hi; cfg < 0 = the library measured faster
                 if m <= m_hi:
                     out = None if cfg < 0 else (cfg, sk)
                     break
-            else:
-                out = _pp_model(m, n, k, mode)
-        else:
-            out = _pp_model(m, n, k, mode)
+        # auto, shape never measured: the library (a hand-written config is routed only on a recorded A/B)
         if out is not None and not _pp_valid(out[0], n, k, mode, out[1]):
             out = None
     _plan_cache[key] = out

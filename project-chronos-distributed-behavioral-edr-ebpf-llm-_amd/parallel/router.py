@@ -5,6 +5,13 @@ collectives in steady state).  The router owns N worker processes — one per GP
 loop and HIP context — and dispatches every request to the replica with the fewest outstanding requests; results
 and streamed tokens come back over a multiprocessing queue.  The HTTP layer sees the same async interface as
 EngineService.
+
+Failover: a supervisor thread watches every worker process.  When one exits (a crash, an OOM kill,
+a GPU fault that took the process down), its in-flight requests are answered at once with an error reply — the
+reference's ERROR verdict path (chronos_sensor.py:121-122) instead of a hang until the client's timeout — the replica
+leaves the routing set, and a FRESH worker process is spawned in its place (never an exec of a process that touched
+the GPU); it rejoins routing when its engine reports ready.  ``/healthz`` shows the transition: "degraded" (503 only
+while no replica is serving) with the dead / restarting replicas and the restart counts.
 """
 from __future__ import annotations
 
@@ -75,35 +82,51 @@ def _worker(rank: int, cfg_dict: dict, req_q, res_q, device: str) -> None:
 
 
 class DPRouter:
-    def __init__(self, cfg, replicas: int, device: str | None = None, start_timeout: float = 900.0):
+    def __init__(self, cfg, replicas: int, device: str | None = None, start_timeout: float = 900.0,
+                 respawn: bool = True, poll_s: float = 0.1):
         self.n = replicas
-        dev = device or ("cuda" if str(cfg.device).startswith("cuda") else "cpu")
-        ctx = mp.get_context("spawn")
-        self._res = ctx.Queue()
-        self._reqs = [ctx.Queue() for _ in range(replicas)]
-        cfgd = asdict(cfg)
-        self._procs = [ctx.Process(target=_worker, args=(r, cfgd, self._reqs[r], self._res, dev), daemon=True)
-                       for r in range(replicas)]
-        for p in self._procs:
-            p.start()
+        self._dev = device or ("cuda" if str(cfg.device).startswith("cuda") else "cpu")
+        self._ctx = mp.get_context("spawn")
+        self._cfgd = asdict(cfg)
+        self._res = self._ctx.Queue()
+        self._reqs = [self._ctx.Queue() for _ in range(replicas)]
+        self._procs = [self._spawn(r) for r in range(replicas)]
         ready = 0
         t0 = time.time()
         while ready < replicas:
             kind, _, _ = self._res.get(timeout=max(1.0, start_timeout - (time.time() - t0)))
             ready += kind == "ready"
         self.outstanding = [0] * replicas
+        self.alive = [True] * replicas       # in the routing set
+        self.restarts = [0] * replicas
+        self.failed_requests = 0
+        self.respawn = respawn
+        self._closing = False
         self._waiters: dict[int, tuple] = {}
         self._rid = itertools.count()
         self._lock = threading.Lock()
         self._reader = threading.Thread(target=self._read, daemon=True)
         self._reader.start()
+        self._poll_s = poll_s
+        self._handled: list = [None] * replicas  # the dead process each replica's last failover handled
+        self._supervisor = threading.Thread(target=self._supervise, daemon=True)
+        self._supervisor.start()
+
+    def _spawn(self, r: int):
+        p = self._ctx.Process(target=_worker, args=(r, self._cfgd, self._reqs[r], self._res, self._dev), daemon=True)
+        p.start()
+        return p
 
     def _read(self) -> None:
         while True:
             try:
                 kind, rid, val = self._res.get()
-            except (EOFError, OSError):
+            except (EOFError, OSError, ValueError):
                 return
+            if kind == "ready":  # a respawned replica rejoins the routing set
+                with self._lock:
+                    self.alive[rid] = True
+                continue
             with self._lock:
                 w = self._waiters.get(rid)
                 if kind == "done":
@@ -115,20 +138,57 @@ class DPRouter:
             loop, sink, _ = w
             loop.call_soon_threadsafe(sink, kind, val)
 
+    def _error_result(self, r: int, msg: str) -> dict:
+        now = time.perf_counter()
+        return dict(text="", error=msg, prompt_ids=0, out_ids=0, done_reason="error", t_submit=now, t_admit=now,
+                    t_first=now, t_done=now, rank=r, meta={"internal_error": True})
+
+    def _supervise(self) -> None:
+        while not self._closing:
+            time.sleep(self._poll_s)
+            for r in range(self.n):
+                p = self._procs[r]
+                if self._closing or p.is_alive():
+                    continue
+                if self._handled[r] is p:  # this death was already handled (respawn off)
+                    continue
+                self._handled[r] = p
+                with self._lock:
+                    self.alive[r] = False
+                    lost = [(rid, w) for rid, w in self._waiters.items() if w[2] == r]
+                    for rid, _ in lost:
+                        del self._waiters[rid]
+                    self.outstanding[r] = 0
+                    self.failed_requests += len(lost)
+                code = p.exitcode
+                for _, (loop, sink, _) in lost:  # answer at once: never leave a caller waiting for a dead replica
+                    loop.call_soon_threadsafe(sink, "done", self._error_result(r, f"replica {r} exited ({code})"))
+                if self.respawn and not self._closing:
+                    self._reqs[r] = self._ctx.Queue()  # whatever the dead worker left queued is answered above
+                    self._procs[r] = self._spawn(r)
+                    self.restarts[r] += 1
+
     def _dispatch(self, params, stream: bool, sink) -> tuple[int, int]:
         loop = asyncio.get_running_loop()
         with self._lock:
-            r = min(range(self.n), key=lambda i: self.outstanding[i])
-            self.outstanding[r] += 1
+            live = [i for i in range(self.n) if self.alive[i]]
             rid = next(self._rid)
-            self._waiters[rid] = (loop, sink, r)
+            if not live:
+                r = -1
+            else:
+                r = min(live, key=lambda i: self.outstanding[i])
+                self.outstanding[r] += 1
+                self._waiters[rid] = (loop, sink, r)
+        if r < 0:  # every replica is down or restarting: the error verdict now, not a hang
+            loop.call_soon(sink, "done", self._error_result(-1, "no replica available (restarting)"))
+            return rid, r
         self._reqs[r].put((rid, asdict(params), stream))
         return rid, r
 
     def _cancel(self, rid: int, r: int) -> None:
         with self._lock:
-            if rid not in self._waiters:
-                return  # already finished
+            if rid not in self._waiters or r < 0:
+                return  # already finished (or failed over)
         self._reqs[r].put(("cancel", rid))
 
     @staticmethod
@@ -176,13 +236,20 @@ class DPRouter:
                 self._cancel(rid, r)
 
     def health(self) -> tuple[bool, dict]:
-        dead = [i for i, p in enumerate(self._procs) if not p.is_alive()]
-        return not dead, {"status": "replica down" if dead else "ok", "dead_replicas": dead}
+        with self._lock:
+            serving = [i for i in range(self.n) if self.alive[i] and self._procs[i].is_alive()]
+            dead = [i for i in range(self.n) if not self._procs[i].is_alive()]
+            restarting = [i for i in range(self.n) if not self.alive[i] and self._procs[i].is_alive()]
+        status = "ok" if len(serving) == self.n else ("degraded" if serving else "down")
+        return bool(serving), {"status": status, "serving_replicas": serving, "dead_replicas": dead,
+                               "restarting_replicas": restarting, "restarts": list(self.restarts),
+                               "failed_over_requests": self.failed_requests}
 
     def info(self) -> dict:
         return {"engines": self.n, "outstanding": list(self.outstanding)}
 
     def close(self) -> None:
+        self._closing = True
         for q in self._reqs:
             q.put("stop")
         for p in self._procs:

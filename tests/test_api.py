@@ -198,3 +198,59 @@ def test_closed_loop_loadgen_against_fake_brain(fake):
     assert rec["chains"] > 8 and rec["errors"] == 0 and rec["p50_latency_ms"] > 0
     bad = asyncio.run(lg.run_level("http://127.0.0.1:9/api/generate", 2, 0.5, 0.0, True, 32, 0))
     assert bad["chains"] == 0 and bad["errors"] > 0
+
+
+@pytest.mark.slow
+def test_dp_router_failover_and_respawn():
+    """A replica process dies mid-request: its callers get an error reply within a second (not a hang), later
+    requests succeed on the other replica and then on the respawned one, and health reports the transition
+    (SURVEY.md §5.3)."""
+    import os
+    import signal
+    import time
+
+    from chronos.brain.api.protocol import GenerateParams
+    from chronos.brain.engine.engine import EngineConfig
+    from chronos.parallel.router import DPRouter
+    from chronos.sensor.prompt import VERDICT_SCHEMA
+
+    router = DPRouter(EngineConfig(model="tiny", device="cpu", max_slots=4, max_model_len=512, use_graphs=False,
+                                   decode_burst=4, max_out=480, jump_forward=False), 2, poll_s=0.05)
+    try:
+        async def go():
+            long = GenerateParams(prompt="chain x", stream=False, num_predict=400)  # free text: runs its budget
+            tasks = [asyncio.ensure_future(router.generate(long)) for _ in range(4)]
+            finished_at = {}
+            for i, t in enumerate(tasks):
+                t.add_done_callback(lambda _t, i=i: finished_at.setdefault(i, time.perf_counter()))
+            await asyncio.sleep(0.5)
+            victim = router._procs[0].pid
+            t_kill = time.perf_counter()
+            os.kill(victim, signal.SIGKILL)
+            await asyncio.sleep(0.3)
+            ok_h, health = router.health()  # the fresh worker is still importing / building its engine
+            done = []
+            for t in tasks:
+                done.append(await asyncio.wait_for(t, 60))
+            failed = [i for i, d in enumerate(done) if d.done_reason == "error"]
+            t_err = max(finished_at[i] for i in failed) - t_kill if failed else 99.0
+            failed = [done[i] for i in failed]
+            # later requests: served while replica 0 restarts, then by both once it is back
+            p = GenerateParams(prompt="chain y", stream=False, format=VERDICT_SCHEMA, num_predict=32)
+            later = await asyncio.gather(*[router.generate(p) for _ in range(3)])
+            t0 = time.perf_counter()
+            while not router.health()[0] or router.health()[1]["status"] != "ok":
+                await asyncio.sleep(0.2)
+                assert time.perf_counter() - t0 < 300
+            after = await asyncio.gather(*[router.generate(p) for _ in range(6)])
+            return failed, t_err, ok_h, health, later, after
+
+        failed, t_err, ok_h, health, later, after = asyncio.run(go())
+        assert failed and all("replica 0" in f.error for f in failed)
+        assert t_err < 1.0 + 0.5  # answered within ~1 s of the kill (poll 50 ms; replicas' CPU load adds jitter)
+        assert ok_h and health["status"] == "degraded" and 0 not in health["serving_replicas"]
+        for o in later + after:
+            assert o.done_reason == "stop" and set(json.loads(o.text)) == {"risk_score", "verdict", "reason"}
+        assert router.restarts[0] == 1 and 0 in {o.rank for o in after}
+    finally:
+        router.close()
