@@ -24,7 +24,8 @@ import time
 from aiohttp import web
 
 from ...utils.metrics import METRICS
-from .protocol import OLLAMA_VERSION, BadRequest, GenerateParams, chat_response, final_fields, generate_response, now_iso
+from .protocol import (OLLAMA_VERSION, BadRequest, GenerateParams, StopFilter, apply_stop, chat_response,
+                       final_fields, generate_response, now_iso)
 
 log = logging.getLogger("chronos.api")
 
@@ -55,17 +56,43 @@ def make_app(backend, model_name: str = "llama3", request_timeout: float | None 
                 # a request the engine rejected is the client's fault (400); a failed engine step is ours (500)
                 internal = (getattr(req, "meta", None) or {}).get("internal_error", False)
                 return web.json_response({"error": req.error}, status=500 if internal else 400)
-            return web.json_response(chat_response(model, req) if chat else generate_response(model, req))
+            if params.stop:  # checked on the finished text: cut at the first stop string, reason "stop"
+                req.text, hit = apply_stop(req.text, params.stop)
+                if hit:
+                    req.done_reason = "stop"
+            return web.json_response(chat_response(model, req) if chat else generate_response(model, req, params.ignored))
         resp = web.StreamResponse(headers={"Content-Type": "application/x-ndjson"})
         await resp.prepare(request)
-        async for text, final in backend.generate_stream(params):
+        sf = StopFilter(params.stop) if params.stop else None
+
+        def piece(text: str, done: bool = False) -> dict:
+            chunk = {"model": model, "created_at": now_iso()}
+            if chat:
+                chunk["message"] = {"role": "assistant", "content": text}
+            else:
+                chunk["response"] = text
+            chunk["done"] = done
+            return chunk
+
+        gen = backend.generate_stream(params)
+        async for text, final in gen:
+            if sf is not None:
+                text = sf.feed(text) if final is None else sf.flush()
+                if final is not None and text:
+                    await resp.write((json.dumps(piece(text)) + "\n").encode())
+                    text = ""
+                if final is None and sf.hit:
+                    # stop string seen: emit what precedes it, end the reply, and close the generator, which
+                    # cancels the engine request (its slot and KV blocks are freed at the next step)
+                    if text:
+                        await resp.write((json.dumps(piece(text)) + "\n").encode())
+                    await gen.aclose()
+                    await resp.write((json.dumps(dict(piece("", True), done_reason="stop")) + "\n").encode())
+                    break
             if final is None:
-                chunk = {"model": model, "created_at": now_iso()}
-                if chat:
-                    chunk["message"] = {"role": "assistant", "content": text}
-                else:
-                    chunk["response"] = text
-                chunk["done"] = False
+                if not text:
+                    continue
+                chunk = piece(text)
             else:
                 if getattr(final, "error", None):
                     chunk = {"error": final.error}
@@ -75,6 +102,7 @@ def make_app(backend, model_name: str = "llama3", request_timeout: float | None 
                         chunk["message"] = {"role": "assistant", "content": ""}
                     else:
                         chunk["response"] = ""
+                        chunk["context"] = [int(t) for t in list(final.prompt_ids) + list(final.out_ids)]
                     chunk.update(final_fields(final))
             await resp.write((json.dumps(chunk) + "\n").encode())
         await resp.write_eof()

@@ -111,7 +111,7 @@ class EngineService:
             handle["req"] = self.engine.submit(
                 ids, fmt=params.format, num_predict=params.num_predict, temperature=params.temperature,
                 seed=params.seed, top_k=params.top_k, top_p=params.top_p, callback=on_done,
-                meta={"on_tokens": on_tokens} if on_tokens else None)
+                meta={"on_tokens": on_tokens} if on_tokens else None, max_len=params.num_ctx or None)
         elif kind == "cancel":
             req = item[1].get("req")
             if req is not None and not req.done_reason:
@@ -131,7 +131,10 @@ class EngineService:
         tok = self.engine.tok
         if params.messages is not None:
             return chat_prompt_ids(tok, params.messages)
-        return tok.chat_ids(params.prompt, system=params.system, raw=params.raw)
+        ids = tok.chat_ids(params.prompt, system=params.system, raw=params.raw)
+        if params.context:  # continuation: the previous exchange's tokens, then this turn (without a second BOS)
+            ids = list(params.context) + (ids[1:] if ids and ids[0] == tok.bos_id else ids)
+        return ids
 
     async def generate(self, params: GenerateParams) -> Request:
         loop = asyncio.get_running_loop()
@@ -290,7 +293,7 @@ class LockstepService(EngineService):
                 return
             handle["tag"] = self.tpe.submit(ids, fmt=params.format, num_predict=params.num_predict,
                                             temperature=params.temperature, seed=params.seed, callback=on_done,
-                                            top_k=params.top_k, top_p=params.top_p)
+                                            top_k=params.top_k, top_p=params.top_p, max_len=params.num_ctx or None)
         elif kind == "cancel":
             tag = item[1].get("tag")
             if tag is not None:

@@ -269,13 +269,15 @@ class Engine:
     def submit(self, prompt: str | list, fmt=None, num_predict: int | None = None, temperature: float = 0.0,
                seed: int = 0, raw: bool = False, system: str | None = None,
                callback: Callable[[Request], None] | None = None, meta: dict | None = None, top_k: int = 0,
-               top_p: float = 1.0) -> Request:
+               top_p: float = 1.0, max_len: int | None = None) -> Request:
         """Queue a request.  A text prompt is tokenized (chat template) lazily at admission, a prefill chunk's worth
         at a time, so host tokenization of a large wave overlaps the GPU prefill of the previous chunk."""
         n = num_predict if num_predict and num_predict > 0 else self.cfg.default_num_predict
         req = Request(next(self._rid), prompt if isinstance(prompt, list) else [], fmt, min(n, self.cfg.max_out),
                       float(temperature or 0.0), int(seed or 0), callback, meta or {})
         req.top_k, req.top_p = int(top_k or 0), float(top_p if top_p is not None else 1.0)
+        if max_len:  # the request's own context window (Ollama options.num_ctx), within the engine's
+            req.meta["max_len"] = min(int(max_len), self.cfg.max_model_len)
         req.t_submit = time.perf_counter()
         try:
             req.start_state = self.bank.get(fmt).start
@@ -295,9 +297,11 @@ class Engine:
         """Clamp num_predict to the context left after the prompt; finish the request with an error if nothing (or
         less than the format's shortest output) fits."""
         ids = req.prompt_ids
-        req.num_predict = n = min(req.num_predict, self.cfg.max_model_len - len(ids))
+        limit = req.meta.get("max_len", self.cfg.max_model_len)
+        req.num_predict = n = min(req.num_predict, limit - len(ids))
         if n <= 0:
-            req.error = f"prompt of {len(ids)} tokens exceeds max_model_len {self.cfg.max_model_len}"
+            what = "num_ctx" if limit < self.cfg.max_model_len else "max_model_len"
+            req.error = f"prompt of {len(ids)} tokens exceeds {what} {limit}"
         elif n < self.bank.min_tokens(req.start_state):
             need = self.bank.min_tokens(req.start_state)
             req.error = f"num_predict={n} cannot fit the shortest output of this format ({need} tokens)"

@@ -40,8 +40,8 @@ def _worker(rank: int, cfg_dict: dict, req_q, res_q, device: str) -> None:
 
     def finish(rid):
         def cb(r):
-            res_q.put(("done", rid, dict(text=r.text, error=r.error, prompt_ids=len(r.prompt_ids),
-                                         out_ids=len(r.out_ids), done_reason=r.done_reason, t_submit=r.t_submit,
+            res_q.put(("done", rid, dict(text=r.text, error=r.error, prompt_ids=list(r.prompt_ids),
+                                         out_ids=list(r.out_ids), done_reason=r.done_reason, t_submit=r.t_submit,
                                          t_admit=r.t_admit, t_first=r.t_first, t_done=r.t_done, rank=rank)))
         return cb
 
@@ -69,9 +69,12 @@ def _worker(rank: int, cfg_dict: dict, req_q, res_q, device: str) -> None:
             p = GenerateParams(**pd)
             ids = chat_prompt_ids(eng.tok, p.messages) if p.messages is not None else \
                 eng.tok.chat_ids(p.prompt, system=p.system, raw=p.raw)
+            if p.context and p.messages is None:
+                ids = list(p.context) + (ids[1:] if ids and ids[0] == eng.tok.bos_id else ids)
             live[rid] = eng.submit(ids, fmt=p.format, num_predict=p.num_predict, temperature=p.temperature,
                                    seed=p.seed, top_k=p.top_k, top_p=p.top_p, callback=finish(rid),
-                                   meta={"rid": rid, **({"on_tokens": tokens(rid)} if stream else {})})
+                                   meta={"rid": rid, **({"on_tokens": tokens(rid)} if stream else {})},
+                                   max_len=p.num_ctx or None)
             try:
                 item = req_q.get_nowait()
             except queue.Empty:
@@ -194,8 +197,9 @@ class DPRouter:
     @staticmethod
     def _result(val: dict) -> SimpleNamespace:
         v = dict(val)
-        v["prompt_ids"] = [0] * v["prompt_ids"]
-        v["out_ids"] = [0] * v["out_ids"]
+        for key in ("prompt_ids", "out_ids"):
+            if isinstance(v[key], int):
+                v[key] = [0] * v[key]
         return SimpleNamespace(**v)
 
     async def generate(self, params):

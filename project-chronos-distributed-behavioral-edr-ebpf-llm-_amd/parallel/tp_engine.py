@@ -38,6 +38,7 @@ class _Sub:
     tag: int = 0
     top_k: int = 0
     top_p: float = 1.0
+    max_len: Optional[int] = None
 
 
 @dataclass
@@ -71,7 +72,8 @@ class TPEngine:
 
     # ---- leader API ----------------------------------------------------------------------------------------------
     def submit(self, prompt, fmt=None, num_predict: int | None = None, temperature: float = 0.0, seed: int = 0,
-               callback: Callable[[Request], None] | None = None, top_k: int = 0, top_p: float = 1.0) -> int:
+               callback: Callable[[Request], None] | None = None, top_k: int = 0, top_p: float = 1.0,
+               max_len: int | None = None) -> int:
         assert self.leader, "requests enter through TP rank 0"
         ids = prompt if isinstance(prompt, list) else self.engine.tok.chat_ids(prompt)
         with self._lock:
@@ -79,7 +81,7 @@ class TPEngine:
             tag = self._tag
             if callback is not None:
                 self._callbacks[tag] = callback
-        self._inbox.put(_Sub(ids, fmt, num_predict, temperature, seed, tag, top_k, top_p))
+        self._inbox.put(_Sub(ids, fmt, num_predict, temperature, seed, tag, top_k, top_p, max_len))
         return tag
 
     def cancel(self, tag: int, reason: str = "cancelled") -> None:
@@ -132,7 +134,8 @@ class TPEngine:
         for s in msg.subs:
             cb = self._callbacks.pop(s.tag, None) if self.leader else None
             r = self.engine.submit(s.ids, fmt=s.fmt, num_predict=s.num_predict, temperature=s.temperature,
-                                   seed=s.seed, callback=cb, meta={"tag": s.tag}, top_k=s.top_k, top_p=s.top_p)
+                                   seed=s.seed, callback=cb, meta={"tag": s.tag}, top_k=s.top_k, top_p=s.top_p,
+                                   max_len=s.max_len)
             if not r.done_reason:
                 self._reqs[s.tag] = r
         for tag, reason in msg.cancels:

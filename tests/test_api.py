@@ -254,3 +254,54 @@ def test_dp_router_failover_and_respawn():
         assert router.restarts[0] == 1 and 0 in {o.rank for o in after}
     finally:
         router.close()
+
+
+def test_stop_filter_unit():
+    from chronos.brain.api.protocol import StopFilter, apply_stop
+
+    assert apply_stop("abc|STOPxyz", ("|STOP", "zz")) == ("abc", True)
+    assert apply_stop("abc", ("q",)) == ("abc", False)
+    f = StopFilter(("|STOP",))
+    out = "".join(f.feed(c) for c in ["ab", "c|S", "TOPxyz", "more"]) + f.flush()
+    assert out == "abc" and f.hit
+    f = StopFilter(("END",))
+    out = "".join(f.feed(c) for c in ["hello ", "wor", "ld E", "N"]) + f.flush()
+    assert out == "hello world EN" and not f.hit
+
+
+def test_ollama_options_stop_num_ctx_context(tiny_service):
+    """options.stop (non-stream and stream), num_ctx (clamp + 400 when the prompt does not fit),
+    keep_alive, context continuation and the reported ignored options."""
+    from chronos.sensor.prompt import VERDICT_SCHEMA
+
+    url = f"{tiny_service.url}/api/generate"
+    base = {"prompt": "chain 1", "format": VERDICT_SCHEMA, "stream": False, "options": {"num_predict": 48}}
+    full = requests.post(url, json=base, timeout=60).json()
+    assert '"verdict"' in full["response"]
+    cut = requests.post(url, json=dict(base, options={"num_predict": 48, "stop": ['"verdict"']}), timeout=60).json()
+    assert cut["response"] == full["response"][:full["response"].index('"verdict"')]
+    assert cut["done_reason"] == "stop"
+    r = requests.post(url, json=dict(base, stream=True, options={"num_predict": 48, "stop": '"verdict"'}),
+                      stream=True, timeout=60)
+    lines = [json.loads(l) for l in r.iter_lines() if l]
+    assert lines[-1]["done"] and "".join(l["response"] for l in lines) == cut["response"]
+
+    # num_ctx: a prompt that does not fit is the client's error; one that fits bounds the generation
+    n_prompt = full["prompt_eval_count"]
+    bad = requests.post(url, json=dict(base, options={"num_ctx": n_prompt - 1}), timeout=60)
+    assert bad.status_code == 400 and "num_ctx" in bad.json()["error"]
+    free = {"prompt": "chain 2", "stream": False, "options": {"num_predict": 64, "num_ctx": n_prompt + 6}}
+    small = requests.post(url, json=free, timeout=60).json()
+    assert small["eval_count"] <= n_prompt + 6 - small["prompt_eval_count"]
+    assert requests.post(url, json=dict(base, options={"num_ctx": -1}), timeout=60).status_code == 400
+
+    # context: the reply's token ids; sending them back continues the conversation (longer prompt)
+    ctx = full["context"]
+    assert len(ctx) == full["prompt_eval_count"] + full["eval_count"]
+    more = requests.post(url, json=dict(base, context=ctx, keep_alive="5m"), timeout=60).json()
+    assert more["prompt_eval_count"] > len(ctx) and set(json.loads(more["response"])) >= {"verdict"}
+    assert requests.post(url, json=dict(base, context="nope"), timeout=60).status_code == 400
+
+    ign = requests.post(url, json=dict(base, options={"num_predict": 48, "repeat_penalty": 1.3,
+                                                      "presence_penalty": 0.0}), timeout=60).json()
+    assert ign["ignored_options"] == ["repeat_penalty"]
