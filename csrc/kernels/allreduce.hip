@@ -337,9 +337,10 @@ struct IpcAllReduce {
             memcpy(&hd, all[p].data(), sizeof(hd));
             memcpy(&hf, all[p].data() + sizeof(hd), sizeof(hf));
             void *pd = nullptr, *pf = nullptr;
+            // recorded as soon as mapped, so a failure on a later peer still unmaps these on destroy
             hip_ok(hipIpcOpenMemHandle(&pd, hd, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle data");
-            hip_ok(hipIpcOpenMemHandle(&pf, hf, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle flags");
             opened.push_back(pd);
+            hip_ok(hipIpcOpenMemHandle(&pf, hf, hipIpcMemLazyEnablePeerAccess), "hipIpcOpenMemHandle flags");
             opened.push_back(pf);
             peers.data[p] = reinterpret_cast<uint16_t*>(pd);
             peers.flags[p] = reinterpret_cast<uint32_t*>(pf);

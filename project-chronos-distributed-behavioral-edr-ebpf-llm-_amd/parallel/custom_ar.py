@@ -16,11 +16,57 @@ flag hop (~5 us, i.e. around half a MiB at ~60 GB/s per link); at W <= 2 it save
 
 A peer that never arrives makes the kernel give up after a bounded spin and set an error word (checked by
 :meth:`check`), rather than hanging the GPU.
+
+Before anything is mapped, :func:`peer_preflight` checks — collectively, so every rank reaches the same answer — that
+each peer's GPU is this process's own device or one it can reach with peer access (``hipDeviceCanAccessPeer``, by
+PCI bus id, so ranks that enumerate devices differently still agree).  If any rank cannot, every rank raises
+:class:`PeerAccessUnavailable` and the caller (``init_tp``) logs the reason and keeps RCCL for all sizes, instead of
+faulting on an unmappable buffer over xGMI.  The handle exchange is agreed the same way: one rank failing to open a
+peer's buffer tears the exchange down on all ranks.
 """
 from __future__ import annotations
 
 import torch
 import torch.distributed as dist
+
+
+class PeerAccessUnavailable(RuntimeError):
+    """The group's GPUs cannot map each other's memory; use RCCL."""
+
+
+def _bus_id(index: int) -> str:
+    p = torch.cuda.get_device_properties(index)
+    return f"{getattr(p, 'pci_domain_id', 0):04x}:{getattr(p, 'pci_bus_id', index):02x}:" \
+           f"{getattr(p, 'pci_device_id', 0):02x}"
+
+
+def _probe(mine: int, peer_bus: str) -> tuple[bool, str]:
+    """Can this process (on device ``mine``) map memory of the GPU with PCI id ``peer_bus``?"""
+    if peer_bus == _bus_id(mine):
+        return True, ""
+    for j in range(torch.cuda.device_count()):
+        if _bus_id(j) == peer_bus:
+            if torch.cuda.can_device_access_peer(mine, j):
+                return True, ""
+            return False, f"no peer access from cuda:{mine} to cuda:{j} ({peer_bus})"
+    return False, f"peer GPU {peer_bus} is not visible to this process"
+
+
+def peer_preflight(group, device: torch.device) -> tuple[bool, str]:
+    """Collective: True on every rank iff every rank can map every peer's GPU memory; else (False, first reason)."""
+    world = dist.get_world_size(group)
+    ids = [None] * world
+    dist.all_gather_object(ids, _bus_id(device.index), group=group)
+    bad = ""
+    for r, bus in enumerate(ids):
+        ok, why = _probe(device.index, bus)
+        if not ok:
+            bad = f"rank {dist.get_rank(group)} -> rank {r}: {why}"
+            break
+    verdicts = [None] * world
+    dist.all_gather_object(verdicts, bad, group=group)
+    reasons = [v for v in verdicts if v]
+    return (not reasons), (reasons[0] if reasons else "")
 
 
 class IpcAllReduce:
@@ -37,14 +83,28 @@ class IpcAllReduce:
         self.max_bytes = max_bytes
         self.spin_limit = spin_limit
         self.two_shot_min_bytes = two_shot_min_bytes
+        self.h = None
+        ok, why = peer_preflight(group, self.device)
+        if not ok:
+            raise PeerAccessUnavailable(why)
         with torch.cuda.device(self.device):
             self.h = self.C.ar_create(self.rank, self.world, max_bytes)
         mine = self.C.ar_handles(self.h)
         allh = [None] * self.world
         dist.all_gather_object(allh, mine.numpy().tobytes(), group=group)
         table = torch.tensor([list(b) for b in allh], dtype=torch.uint8)
-        with torch.cuda.device(self.device):
-            self.C.ar_open(self.h, table)
+        err = ""
+        try:
+            with torch.cuda.device(self.device):
+                self.C.ar_open(self.h, table)
+        except RuntimeError as e:
+            err = f"rank {self.rank}: {e}"
+        errs = [None] * self.world
+        dist.all_gather_object(errs, err, group=group)
+        errs = [e for e in errs if e]
+        if errs:
+            self.close()
+            raise PeerAccessUnavailable(f"IPC handle exchange failed ({errs[0]})")
         self.capacity = self.C.ar_capacity(self.h)  # elements per parity half
 
     def fits(self, x: torch.Tensor) -> bool:

@@ -178,8 +178,10 @@ def init_tp(backend: str = "nccl", ipc_allreduce: bool | None = None) -> tuple[T
     if ipc_allreduce is None:
         ipc_allreduce = backend == "nccl" and os.environ.get("CHRONOS_IPC_ALLREDUCE", "1") != "0"
     if ipc_allreduce and tp.world > 1:
-        try:
+        from .custom_ar import PeerAccessUnavailable
+
+        try:  # collective: every rank gets the same outcome (custom_ar.peer_preflight)
             tp.enable_ipc_allreduce()
-        except Exception as e:  # noqa: BLE001 — reported, and RCCL remains a complete implementation
+        except PeerAccessUnavailable as e:  # reported, and RCCL remains a complete implementation
             logging.getLogger("chronos.tp").warning("IPC all-reduce unavailable (%s); using RCCL only", e)
     return tp, ctrl

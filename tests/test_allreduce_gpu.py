@@ -54,12 +54,13 @@ def _expected(world, step, n):
     return acc.to(torch.bfloat16)
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, distinct=False):
+    """``distinct``: rank r on cuda:r (peer mapping over xGMI, tests/test_multi_gpu.py); else all ranks on cuda:0."""
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.cuda.set_device(0)
+    torch.cuda.set_device(rank if distinct else 0)
     from chronos.parallel.custom_ar import IpcAllReduce
 
     res = {"ok": True, "msg": ""}
