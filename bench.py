@@ -9,10 +9,12 @@ independent Brain engine — the DP-replica deployment of SURVEY.md §2.5 — on
          (<= --num-predict tokens, the reference's ~60-token replies) for every chain, detokenizes and the verdict
          is parsed with json.loads, exactly as the sensor does (chronos_sensor.py:120).
 
-``--mode closed`` (opt-in) measures the same metric in steady state instead of waves: every one of the ``--streams``
-sensor streams keeps exactly one chain in flight and submits its next chain the moment its verdict returns, so a
-step is ``--streams`` completed chains with no wave boundary (no straggler tail, the prefix cache stays warm as in a
-long-running server).  The default remains the wave form above.
+``--mode closed`` measures the same metric in steady state instead of waves: every one of the ``--streams`` sensor
+streams keeps exactly one chain in flight and submits its next chain the moment its verdict returns, so a step is
+``--streams`` completed chains with no wave boundary (no straggler tail; new prompts are prefilled in the same forward
+as the live decode rows — mixed steps — and the prefix cache stays warm as in a long-running server).  The headline
+stays the wave form above; after it, ``--closed-steps`` closed-loop steps are timed too and reported as
+``closed_loop_chains_s`` / ``closed_loop_p50_ms`` / ``closed_loop_p99_ms`` in the same JSON line.
 
 Weights are random-init Llama-3-8B (real architecture, bf16, no checkpoint offline); data is synthetic telemetry.
 Work per GPU is fixed as N grows (weak scaling).  Rank 0 prints ONE JSON line.
@@ -59,6 +61,9 @@ def parse():
     ap.add_argument("--prefill-ramp", type=int, default=2048, help="first prefill step after idle (0 = full chunks)")
     ap.add_argument("--no-jump-forward", action="store_true", help="decode grammar-forced runs token by token")
     ap.add_argument("--mode", choices=["wave", "closed"], default="wave")
+    ap.add_argument("--closed-steps", type=int, default=2,
+                    help="wave mode: afterwards also time this many closed-loop steps (steady-state arrivals) and "
+                         "report them as closed_loop_* next to the headline (0 = skip)")
     ap.add_argument("--weights", choices=["bf16", "fp8"], default="bf16",
                     help="fp8 = W8A8 e4m3 projections on the block-scaled MFMA / hipBLASLt fp8 (not the headline)")
     ap.add_argument("--device", default="cuda")
@@ -71,11 +76,13 @@ def parse():
     return ap.parse_args()
 
 
-def run_closed(a, eng, prompts, barrier, progress):
+def run_closed(a, eng, prompts, barrier, progress, steps=None, warmup=None):
     """Steady state: each stream resubmits on completion.  Returns (elapsed, timed requests, prefix-hit tokens)."""
     from chronos.sensor.prompt import VERDICT_SCHEMA
 
-    done, nxt, stop = [], [0], [False]
+    steps = a.steps if steps is None else steps
+    warmup = a.warmup if warmup is None else warmup
+    done, stop = [], [False]
     # each stream's chains come from its own slice, so no prompt is ever submitted twice
     per = len(prompts) // a.streams
     pos = [0] * a.streams
@@ -94,13 +101,13 @@ def run_closed(a, eng, prompts, barrier, progress):
 
     for s in range(a.streams):
         submit(s)
-    while len(done) < a.warmup * a.streams and eng.has_work():
+    while len(done) < warmup * a.streams and eng.has_work():
         eng.step()
     progress(f"closed-loop warmup: {len(done)} chains {dict(eng.stats)}")
     barrier()
     n0, hit0 = len(done), eng.stats["prefix_hit_tokens"]
     t0 = time.perf_counter()
-    target = n0 + a.steps * a.streams
+    target = n0 + steps * a.streams
     while len(done) < target and eng.has_work():
         eng.step()
     barrier()
@@ -188,8 +195,10 @@ def main():
     eng = Engine(cfg, tp=tp)
     total_steps = a.warmup + a.steps
     per_stream = total_steps if a.mode == "wave" else 2 * total_steps + 2  # closed loop: fast streams cycle more
-    chains = synthetic_chains(a.streams * per_stream + a.single_stream, seed=1000 + replica)
+    closed_per = 2 * (1 + a.closed_steps) + 2 if a.mode == "wave" and a.closed_steps > 0 else 0
+    chains = synthetic_chains(a.streams * (per_stream + closed_per) + a.single_stream, seed=1000 + replica)
     prompts = [build_prompt(c.history) for c in chains]
+    n_main, n_closed = a.streams * per_stream, a.streams * closed_per
 
     def run_step(batch):
         # Nothing computed outside a step is reused inside it: the prefix cache starts empty every step, so only
@@ -243,9 +252,17 @@ def main():
     progress("verdict length histogram (4-token bins): " + json.dumps(dict(sorted(hist.items()))))
     prompt_tok = sum(len(r.prompt_ids) for r in timed)
 
+    closed = None
+    if closed_per:  # steady-state arrivals after the wave headline
+        eng.blocks.clear_cache()
+        c_el, c_timed, _ = run_closed(a, eng, prompts[n_main:n_main + n_closed], barrier, progress,
+                                      steps=a.closed_steps, warmup=1)
+        closed = dict(elapsed=c_el, n=len(c_timed), lat=[r.latency for r in c_timed])
+        progress(f"closed loop: {len(c_timed)} chains in {c_el:.2f}s")
+
     # single-stream latency (the reference's regime: one chain in flight)
     single = []
-    for p in prompts[a.streams * per_stream:]:
+    for p in prompts[n_main + n_closed:]:
         single += run_step([p])
     single_lat = [r.latency for r in single[1:]] or [r.latency for r in single]
     # per-token decode time of the single stream: independent of how long the random-weight verdicts happen to be
@@ -253,7 +270,7 @@ def main():
     single_tok = [((r.t_done - r.t_first), len(r.out_ids)) for r in ss if r.t_first]
 
     stats = dict(elapsed=elapsed, ok=ok, n=len(timed), lat=lat, gen=gen_tok, ptok=prompt_tok, single=single_lat,
-                 single_tok=single_tok, hits=hits, tp_rank=tp_rank)
+                 single_tok=single_tok, hits=hits, tp_rank=tp_rank, closed=closed)
     if world > 1:
         allst = [None] * world
         dist.all_gather_object(allst, stats)
@@ -261,6 +278,7 @@ def main():
         allst = [stats]
     if rank == 0:
         t = max(s["elapsed"] for s in allst)
+        c_t = max(s["closed"]["elapsed"] for s in allst) if allst[0]["closed"] else 0.0
         allst = [s for s in allst if s["tp_rank"] == 0]  # one report per replica (its TP ranks served the same chains)
         n = sum(s["n"] for s in allst)
         oks = sum(s["ok"] for s in allst)
@@ -307,6 +325,12 @@ def main():
             "generated_tokens_per_s": round(sum(s["gen"] for s in allst) / t, 1),
             "prefix_cache_hit_fraction": round(sum(s["hits"] for s in allst) / max(1, sum(s["ptok"] for s in allst)), 3),
         }
+        if allst[0]["closed"]:
+            c_lat = sorted(x for s in allst for x in s["closed"]["lat"])
+            out.update(closed_loop_chains_s=round(sum(s["closed"]["n"] for s in allst) / c_t, 3),
+                       closed_loop_p50_ms=round(1000 * statistics.median(c_lat), 2),
+                       closed_loop_p99_ms=round(1000 * c_lat[max(0, math.ceil(0.99 * len(c_lat)) - 1)], 2),
+                       closed_loop_steps=a.closed_steps)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
