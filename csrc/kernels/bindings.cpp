@@ -473,6 +473,19 @@ Tensor gemm(const Tensor& x, const Tensor& w, bool swiglu, int64_t stages) {
     return y;
 }
 
+// Split-K tickets: one zeroed int buffer per (device, stream), at least n long; every call leaves it zeroed (each
+// group's last arriver resets its own counter), so calls on one stream — and graph replays — share it.
+static int32_t* split_tickets(const Tensor& x, int64_t n) {
+    static std::mutex mu;
+    static std::unordered_map<int64_t, Tensor> cnts;
+    std::lock_guard<std::mutex> lk(mu);
+    const int64_t key = ((int64_t)x.get_device() << 48) ^ (int64_t)(intptr_t)cur_stream();
+    auto it = cnts.find(key);
+    if (it == cnts.end() || it->second.numel() < n)
+        it = cnts.insert_or_assign(key, at::zeros({std::max<int64_t>(n, 1 << 16)}, x.options().dtype(at::kInt))).first;
+    return it->second.data_ptr<int32_t>();
+}
+
 // Batched projection GEMM family (gemm_pp.hip): y = x @ w.T with a fused epilogue, M >= 3.
 //   mode 0 plain (y [M, N]); 1 swiglu (w = [gate; up] [2F, K], y [M, F] = silu(x Wg^T) * (x Wu^T)); 2 resid (y = the
 //   new residual stream bf16(bf16(x @ w.T) + resid), second output = per-row partial sums of y^2 [M, N / (BN/4)]).
@@ -527,18 +540,65 @@ std::tuple<Tensor, Tensor> gemm_pp(const Tensor& x, const Tensor& w, int64_t mod
     if (splitk > 1) {
         ws = at::empty({tiles * splitk * BM * BN}, x.options().dtype(at::kFloat));
         a.ws = ws.data_ptr<float>();
-        // tickets: one zeroed buffer per (device, stream); every call leaves it zeroed (the last arriver resets)
-        static std::mutex mu;
-        static std::unordered_map<int64_t, Tensor> cnts;
-        std::lock_guard<std::mutex> lk(mu);
-        const int64_t key = ((int64_t)x.get_device() << 48) ^ (int64_t)(intptr_t)cur_stream();
-        auto it = cnts.find(key);
-        if (it == cnts.end() || it->second.numel() < tiles)
-            it = cnts.insert_or_assign(key, at::zeros({std::max<int64_t>(tiles, 1 << 16)},
-                                                       x.options().dtype(at::kInt))).first;
-        a.cnt = it->second.data_ptr<int32_t>();
+        a.cnt = split_tickets(x, tiles);
     }
     CHK(chronos::launch_gemm_pp((int)cfg, (int)mode, part_in.has_value(), prio, a, cur_stream()), "gemm_pp: launch");
+    return {y, part_out};
+}
+
+// Skinny-M GEMM (gemm_skinny.hip), M <= 16 * MT of the config: same epilogues and tensors as gemm_pp; the kResid
+// partials are [M, N / (16 * RT)].
+std::tuple<Tensor, Tensor> gemm_skinny(const Tensor& x, const Tensor& w, int64_t mode, int64_t cfg, int64_t splitk,
+                                       const c10::optional<Tensor>& resid, const c10::optional<Tensor>& part_in,
+                                       double eps) {
+    chk_bf16(x, "x");
+    chk_bf16(w, "w");
+    const int64_t K = x.size(-1), M = x.numel() / K, N = w.size(0);
+    CHK(w.dim() == 2 && w.size(1) == K, "gemm_skinny: w must be [N, K]");
+    CHK(cfg >= 0 && cfg < chronos::kSkinnyConfigs, "gemm_skinny: cfg");
+    CHK(mode >= 0 && mode <= 2, "gemm_skinny: mode");
+    const int RT = chronos::gemm_skinny_rt((int)cfg), MT = chronos::gemm_skinny_mt((int)cfg);
+    CHK(M >= 1 && M <= 16 * MT, "gemm_skinny: M must be in [1, 16 * MT] of the config");
+    CHK(splitk >= 1 && K % (256 * splitk) == 0 && K <= (1 << 20) && N * K < (1LL << 40),
+        "gemm_skinny: K % (256 * splitk) == 0");
+    CHK(mode == 1 ? RT % 2 == 0 && (N / 2) % (8 * RT) == 0 && N % 2 == 0 : N % (16 * RT) == 0,
+        "gemm_skinny: N % (16 RT) (swiglu: F % (8 RT), RT even)");
+    CHK(mode != 2 || !part_in.has_value(), "gemm_skinny: resid mode has no norm prologue");
+    c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
+    chronos::PPArgs a{};
+    a.x = bf(x);
+    a.w = bf(w);
+    a.M = (int)M;
+    a.N = (int)N;
+    a.K = (int)K;
+    a.F = (int)(N / 2);
+    a.splitk = (int)splitk;
+    a.eps = (float)eps;
+    Tensor y = at::empty({M, mode == 1 ? N / 2 : N}, x.options());
+    a.y = bfm(y);
+    Tensor part_out;
+    if (mode == 2) {
+        CHK(resid.has_value(), "gemm_skinny: resid mode needs resid");
+        chk_bf16(*resid, "resid");
+        CHK(resid->numel() == M * N, "gemm_skinny: resid must be [M, N]");
+        a.resid = bf(*resid);
+        part_out = at::empty({M, N / (16 * RT)}, x.options().dtype(at::kFloat));
+        a.part_out = part_out.data_ptr<float>();
+    }
+    if (part_in.has_value()) {
+        chk_gpu(*part_in, "part_in");
+        CHK(part_in->scalar_type() == at::kFloat && part_in->dim() == 2 && part_in->size(0) == M, "part_in [M, P] f32");
+        a.part_in = part_in->data_ptr<float>();
+        a.nparts_in = (int)part_in->size(1);
+    }
+    const int64_t groups = mode == 1 ? (N / 2) / (8 * RT) : N / (16 * RT);
+    Tensor ws;
+    if (splitk > 1) {
+        ws = at::empty({groups * splitk * 64 * RT * MT * 4}, x.options().dtype(at::kFloat));
+        a.ws = ws.data_ptr<float>();
+        a.cnt = split_tickets(x, groups);
+    }
+    CHK(chronos::launch_gemm_skinny((int)cfg, (int)mode, part_in.has_value(), a, cur_stream()), "gemm_skinny: launch");
     return {y, part_out};
 }
 
@@ -661,6 +721,8 @@ TORCH_LIBRARY(chronos, m) {
     m.def("gemv(Tensor x, Tensor w, bool swiglu) -> Tensor");
     m.def("gemm(Tensor x, Tensor w, bool swiglu, int stages=3) -> Tensor");
     m.def("gemm_pp(Tensor x, Tensor w, int mode, int cfg, int splitk, Tensor? resid, Tensor? part_in, float eps, bool prio) -> (Tensor, Tensor)");
+    m.def("gemm_skinny(Tensor x, Tensor w, int mode, int cfg, int splitk, Tensor? resid, Tensor? part_in, float eps) "
+          "-> (Tensor, Tensor)");
     m.def("gemv_resid(Tensor x, Tensor w, Tensor resid_in, Tensor(a!) resid_out) -> Tensor");
     m.def("gemv_normp(Tensor s, Tensor part, float eps, Tensor w, bool swiglu) -> Tensor");
     m.def("qkv_rope(Tensor x, Tensor? part, float eps, Tensor w, Tensor pos, Tensor tok_seq, "
@@ -699,6 +761,7 @@ TORCH_LIBRARY_IMPL(chronos, CUDA, m) {
     m.impl("gemv", &gemv);
     m.impl("gemm", &gemm);
     m.impl("gemm_pp", &gemm_pp);
+    m.impl("gemm_skinny", &gemm_skinny);
     m.impl("gemv_resid", &gemv_resid);
     m.impl("gemv_normp", &gemv_normp);
     m.impl("qkv_rope", &qkv_rope);

@@ -5,11 +5,13 @@ Routing is by measured shape:
 
 * M <= 2 (single-stream decode): the hand-written GEMV (csrc/kernels/gemv.hip), 1 KiB row-contiguous weight
   streaming — beats hipBLASLt on every decode shape;
-* M >= 3: the hand-written ping-pong MFMA GEMM family (csrc/kernels/gemm_pp.hip) with its fused epilogues — the
-  decoder's residual add + RMSNorm partial sums on O / down (``pp_resid`` -> ResidOut), the folded RMSNorm as a
-  per-row scale on QKV / gate_up / LM head (a LazyNorm input), SwiGLU on gate_up — with the tile config and split-K
-  of the measured plan (``gemm_plan.json``: per (N, K, epilogue) the best of the configs by M range, from
-  ``scripts/bench_gemm_pp.py`` on one MI355X, random operands, cold weights);
+* M >= 3: the hand-written MFMA GEMM families with their fused epilogues — the decoder's residual add + RMSNorm
+  partial sums on O / down (``gemv_resid`` -> ResidOut), the folded RMSNorm as a per-row scale on QKV / gate_up / LM
+  head (a LazyNorm input), SwiGLU on gate_up: the skinny-M weight-streaming kernel (csrc/kernels/gemm_skinny.hip,
+  M <= 64: jump-forward forwards, tail decode buckets) and the ping-pong tile GEMM (csrc/kernels/gemm_pp.hip) above,
+  with the kernel, tile config and split-K of the measured plan (``gemm_plan.json``: per (N, K, epilogue) the best
+  by M range, from ``scripts/tune_gemm_pp.py`` on one MI355X, random operands, cold weights; plan cfg >= 100 is
+  skinny config cfg - 100);
 * hipBLASLt (torch.matmul) only where the plan records that the library wins by more than 3 % (the "plain library
   GEMM" rule), or for shapes the kernel does not take (K % 64, N % 4).  CHRONOS_PP=lib|own|auto forces a side.
 """
@@ -31,6 +33,10 @@ _PP_BM = {0: 256, 1: 128, 2: 256, 3: 128, 4: 256, 5: 128, 6: 256, 7: 128, 8: 256
 _PP_BN = {0: 256, 1: 256, 2: 128, 3: 128, 4: 256, 5: 256, 6: 128, 7: 128, 8: 256, 9: 256, 10: 128, 11: 128}
 # relative per-CU MAC rate of each tile config at full occupancy (gate_up M = 1024 sweep, profiles/r3_gemm_pp_*)
 _PP_RATE = {0: 1.0, 1: 0.84, 2: 0.84, 3: 0.66, 4: 1.0, 5: 0.71, 6: 0.73, 7: 0.6, 8: 1.0, 9: 0.84, 10: 0.84, 11: 0.66}
+# skinny-M configs (gemm_skinny.hip SK_CONFIGS): plan id SK_BASE + c -> (RT: W tiles of 16 rows, MT: M <= 16 MT)
+SK_BASE = 100
+_SK = {0: (1, 1), 1: (2, 1), 2: (4, 1), 3: (2, 2), 4: (4, 2), 5: (2, 4), 6: (4, 4)}
+SKINNY_MAX_M = 64
 _plan_cache: dict = {}
 _plan_table: Optional[dict] = None
 
@@ -50,7 +56,33 @@ def _plan_file() -> dict:
     return _plan_table
 
 
-def _pp_valid(cfg: int, n: int, k: int, mode: int, sk: int) -> bool:
+def _sk_valid(c: int, m: int, n: int, k: int, mode: int, sk: int) -> bool:
+    rt, mt = _SK[c]
+    if m > 16 * mt or k % (256 * sk):
+        return False
+    return (rt % 2 == 0 and n % 2 == 0 and (n // 2) % (8 * rt) == 0) if mode == PP_SWIGLU else n % (16 * rt) == 0
+
+
+def _sk_model(m: int, n: int, k: int, mode: int, cus: int = 256) -> Optional[tuple[int, int]]:
+    """Cost-model pick of a skinny config: the narrowest x tile covering M, W tiles >= x tiles (x re-read bytes <=
+    weight bytes), split-K until the grid covers the CUs twice."""
+    best = None
+    for c, (rt, mt) in _SK.items():
+        if m > 16 * mt or (mt > 1 and m <= 8 * mt):
+            continue
+        groups = (n // 2) // (8 * rt) if mode == PP_SWIGLU else n // (16 * rt)
+        for sk in (1, 2, 4, 7, 8, 14, 16):
+            if not _sk_valid(c, m, n, k, mode, sk):
+                continue
+            t = (rt < mt, -min(groups * sk, 2 * cus), sk, -rt)
+            if best is None or t < best[0]:
+                best = (t, (SK_BASE + c, sk))
+    return best[1] if best else None
+
+
+def _pp_valid(cfg: int, n: int, k: int, mode: int, sk: int, m: int = 0) -> bool:
+    if cfg >= SK_BASE:
+        return cfg - SK_BASE in _SK and _sk_valid(cfg - SK_BASE, m, n, k, mode, sk)
     bn = _PP_BN[cfg]
     if k % 64 or (k // 64) % sk:
         return False
@@ -75,7 +107,8 @@ def _pp_model(m: int, n: int, k: int, mode: int, cus: int = 256) -> tuple[int, i
 
 
 def pp_plan(m: int, n: int, k: int, mode: int = PP_PLAIN) -> Optional[tuple[int, int]]:
-    """(tile config, split-K) of the hand-written batched GEMM for this shape, or None for the library."""
+    """(config, split-K) of the hand-written batched GEMM for this shape — config >= SK_BASE is the skinny kernel —
+    or None for the library."""
     if m < 3 or PP_MODE == "lib":
         return None
     key = (m, n, k, mode)
@@ -86,14 +119,14 @@ def pp_plan(m: int, n: int, k: int, mode: int = PP_PLAIN) -> Optional[tuple[int,
     if k % 64 == 0 and (n % 4 == 0 if mode == PP_PLAIN else n % 128 == 0):
         rows = _plan_file().get((n, k, mode))
         if PP_MODE == "own":
-            out = _pp_model(m, n, k, mode)
+            out = (_sk_model(m, n, k, mode) if m <= SKINNY_MAX_M else None) or _pp_model(m, n, k, mode)
         elif rows:
-            for m_hi, cfg, sk in rows:  # sorted by m_hi; cfg < 0 = the library measured faster
-                if m <= m_hi:
-                    out = None if cfg < 0 else (cfg, sk)
-                    break
+            # rows [measured M, cfg, split-K] sorted by M: a measured M decides (previous M, M]; the last row also
+            # everything above it.  cfg < 0 = the library measured faster.
+            pick = next((r for r in rows if m <= r[0]), rows[-1])
+            out = None if pick[1] < 0 else (pick[1], pick[2])
         # auto, shape never measured: the library (a hand-written config is routed only on a recorded A/B)
-        if out is not None and not _pp_valid(out[0], n, k, mode, out[1]):
+        if out is not None and not _pp_valid(out[0], n, k, mode, out[1], m):
             out = None
     _plan_cache[key] = out
     return out
@@ -101,10 +134,13 @@ def pp_plan(m: int, n: int, k: int, mode: int = PP_PLAIN) -> Optional[tuple[int,
 
 def pp_gemm(x: torch.Tensor, w: torch.Tensor, mode: int, plan: tuple[int, int], resid=None, part=None,
             eps: float = 1e-5):
-    """One launch of gemm_pp.hip: returns (y, partials) — partials only for the residual epilogue."""
+    """One launch of gemm_pp.hip (or gemm_skinny.hip for a skinny plan): returns (y, partials) — partials only for
+    the residual epilogue."""
     from . import _k
 
     k = x.shape[-1]
+    if plan[0] >= SK_BASE:
+        return _k().gemm_skinny(x.reshape(-1, k), w, mode, plan[0] - SK_BASE, plan[1], resid, part, eps)
     y, pt = _k().gemm_pp(x.reshape(-1, k), w, mode, plan[0], plan[1], resid, part, eps, False)
     return y, pt
 

@@ -1,7 +1,8 @@
-"""Measure the batched GEMM family (gemm_pp.hip) against hipBLASLt on every projection shape of the served models and
-write the routing plan ops/gemm_plan.json (+ a per-shape table for profiles/).
+"""Measure the hand-written GEMM families (gemm_skinny.hip for M <= 64, gemm_pp.hip) against hipBLASLt on every
+projection shape of the served models and write the routing plan ops/gemm_plan.json (+ a per-shape table for
+profiles/; M <= 2 rows record the decode GEMV, gemv.hip, which is always routed there).
 
-For each (N, K, epilogue) and each M bucket: the fastest tile config / split-K among the cost model's candidates,
+For each (N, K, epilogue) and each M bucket: the fastest kernel / config / split-K among the cost model's candidates,
 timed interleaved with the library path of the same epilogue (library GEMM + silu_mul for SwiGLU, + the residual add
 for the residual epilogue) in one process on cold weights (cdna_hip_programming.md §5.4 rule 24).  The plan keeps
 the hand-written kernel unless the library is more than 3 % faster (any shape left on the library needs a
@@ -26,7 +27,22 @@ SHAPES = {
     "70b-tp8": {"qkv": (1280, 8192, 0), "o": (8192, 1024, 0), "gate_up": (7168, 8192, 1), "down": (8192, 3584, 0),
                 "lm_head": (16032, 8192, 0)},
 }
-MS = [3, 8, 16, 32, 64, 128, 256, 512, 768, 1024, 2048, 4096, 8192, 16384]
+MS = [1, 2, 3, 4, 5, 8, 16, 32, 48, 64, 128, 256, 512, 768, 1024, 2048, 4096, 8192, 16384]
+
+
+def skinny_candidates(m, n, k, mode, keep=8):
+    from chronos.ops import gemm as G
+
+    out = []
+    for c, (rt, mt) in G._SK.items():
+        if m > 16 * mt or (mt > 1 and m <= 8 * mt and mt != 2):
+            continue
+        groups = (n // 2) // (8 * rt) if mode == 1 else n // (16 * rt)
+        for sk in (1, 2, 3, 4, 7, 8, 14, 16):
+            if G._sk_valid(c, m, n, k, mode, sk) and 192 <= groups * sk <= 4096 and (sk == 1 or groups < 1024):
+                out.append((groups * sk, G.SK_BASE + c, sk))
+    out.sort(key=lambda t: abs(t[0] - 768))
+    return [(c, sk) for _, c, sk in out[:keep]]
 
 
 def candidates(m, n, k, mode, keep=6):
@@ -60,8 +76,14 @@ def main():
     ap.add_argument("--iters", type=int, default=8)
     ap.add_argument("--out-plan", default="")
     ap.add_argument("--out-table", default="")
+    ap.add_argument("--merge", default="", help="plan file whose rows at M not measured in this run are kept")
     args = ap.parse_args()
+    merged = {}
+    if args.merge:
+        with open(args.merge) as fh:
+            merged = json.load(fh).get("plans", {})
     from chronos import ops
+    from chronos.ops import gemm as G
 
     ops.load()
     dev = "cuda"
@@ -86,9 +108,22 @@ def main():
                     return ops.silu_mul(y) if mode == 1 else (y + resid if mode == 2 else y)
 
                 def own(i, c):
+                    if c[0] == "gemv":
+                        if mode == 2:
+                            return G.gemv_resid(x, ws[i % ncopy], resid).s
+                        return G._gemv(x, ws[i % ncopy], mode == 1)
+                    if c[0] >= G.SK_BASE:
+                        return torch.ops.chronos.gemm_skinny(x, ws[i % ncopy], mode, c[0] - G.SK_BASE, c[1], resid,
+                                                             None, 1e-5)[0]
                     return torch.ops.chronos.gemm_pp(x, ws[i % ncopy], mode, c[0], c[1], resid, None, 1e-5, False)[0]
 
-                cands = candidates(m, n, k, mode)
+                if m <= 2:
+                    if not G.gemv_ok(m, n, k):
+                        continue
+                    cands = [("gemv", 1)]
+                else:
+                    cands = (skinny_candidates(m, n, k, mode) if m <= G.SKINNY_MAX_M else []) + \
+                        (candidates(m, n, k, mode) if m >= 16 else [])
                 ref = lib(0).float()
                 scale = ref.abs().max().item() + 1e-6
                 bad = [c for c in cands if (own(0, c).float() - ref).abs().max().item() > 0.03 * scale]
@@ -110,22 +145,30 @@ def main():
                 best = min(cands, key=lambda c: min(times[c]))
                 lib_us, own_us = min(times["lib"]), min(times[best])
                 use_lib = lib_us < own_us / 1.03
-                rows.append([m, -1 if use_lib else best[0], 1 if use_lib else best[1]])
+                if m > 2:
+                    rows.append([m, -1 if use_lib else best[0], 1 if use_lib else best[1]])
+                wbytes = n * k * 2
                 rec = dict(model=model, op=op, m=m, n=n, k=k, mode=mode, lib_us=round(lib_us, 2),
                            own_us=round(own_us, 2), own=f"cfg{best[0]}_sk{best[1]}",
                            lib_TF=round(flop / lib_us / 1e6, 1), own_TF=round(flop / own_us / 1e6, 1),
-                           speedup=round(lib_us / own_us, 3), route="lib" if use_lib else "own",
+                           own_weight_TBs=round(wbytes / own_us / 1e6, 2), lib_weight_TBs=round(wbytes / lib_us / 1e6, 2),
+                           speedup=round(lib_us / own_us, 3), route="lib" if use_lib and m > 2 else "own",
                            all={f"cfg{c[0]}_sk{c[1]}": round(min(times[c]), 2) for c in cands})
                 table.append(rec)
                 print(json.dumps(rec), flush=True)
-            # plan rows: a measured M decides (previous measured M, M] (its tiles cover any M up to it); the last
-            # one also everything above
-            keyed = [[m if i + 1 < len(rows) else 1 << 30, cfg, sk] for i, (m, cfg, sk) in enumerate(rows)]
-            plans[f"{n},{k},{mode}"] = keyed
+            # plan rows [measured M, cfg, split-K]: ops/gemm.py routes (previous measured M, M] by the row of M and
+            # everything above the last row by the last row; rows of an earlier plan (--merge) at other M are kept
+            key = f"{n},{k},{mode}"
+            old = {r[0]: r for r in merged.get(key, []) if r[0] < (1 << 30)}
+            old.update({r[0]: r for r in rows})
+            plans[key] = [old[m] for m in sorted(old)]
             del ws
             torch.cuda.empty_cache()
-    meta = {"device": torch.cuda.get_device_name(0), "note": "rows: [M upper bound, cfg (-1 = library), split-K]"}
+    meta = {"device": torch.cuda.get_device_name(0),
+            "note": "rows: [measured M, cfg (-1 = library, >= 100 = skinny config cfg - 100), split-K]"}
     if args.out_plan:
+        for key, rows in merged.items():  # shapes not measured in this run
+            plans.setdefault(key, rows)
         with open(args.out_plan, "w") as fh:
             json.dump({"meta": meta, "plans": plans}, fh, indent=1)
     if args.out_table:
