@@ -1,4 +1,4 @@
-// gemm_skinny.hip — skinny-M projection GEMM (M = 3..64 rows): jump-forward forwards, the tail decode buckets and
+// gemm_skinny.hip — skinny-M projection GEMM (M = 3..128 rows): jump-forward forwards, the tail decode buckets and
 // 70B TP=8 per-GPU decode (SURVEY.md §2.3 K3/K7/K8/K10/K11, §7.3 hard part 1; VERDICT r2 "skinny-M GEMM").
 //
 //   y[M, N] = x[M, K] · W[N, K]^T   (bf16 in, fp32 accumulate) with the batched family's epilogues (chronos_gemm.h):
@@ -11,7 +11,7 @@
 //     units (wave w takes units w, w+4, ...), so the main loop has no barrier and no LDS at all;
 //   * W goes straight from HBM into VGPRs in the v_mfma_f32_16x16x32_bf16 A layout (lane l: row l&15, k 8(l>>4)..+8
 //     of each 32-k block).  A unit is two such loads per A tile, i.e. one full 128-B line of each of 16 rows;
-//     x (L2-resident: <= 64 x K bf16) comes the same way as the B operand (column = x row l&15), rows >= M clamped;
+//     x (L2-resident: <= 128 x K bf16) comes the same way as the B operand (column = x row l&15), rows >= M clamped;
 //   * a register ring D units deep keeps D * RT KiB of weights in flight per wave (in-order vmcnt: the compiler's
 //     counted waits retire the oldest unit only);
 //   * MT x tiles of 16 rows (M <= 16 MT), RT W tiles: x bytes / W bytes = MT / RT per wave, kept <= 2 so the TCP
@@ -257,7 +257,8 @@ void launch_cfg(const PPArgs& a, hipStream_t st) {
     X(3, 2, 2, 4)     \
     X(4, 4, 2, 3)     \
     X(5, 2, 4, 3)     \
-    X(6, 4, 4, 2)
+    X(6, 4, 4, 2)     \
+    X(7, 2, 8, 2)
 
 template <int MODE, bool NORMP>
 bool launch_mode(int cfg, const PPArgs& a, hipStream_t st) {

@@ -8,7 +8,7 @@ Routing is by measured shape:
 * M >= 3: the hand-written MFMA GEMM families with their fused epilogues — the decoder's residual add + RMSNorm
   partial sums on O / down (``gemv_resid`` -> ResidOut), the folded RMSNorm as a per-row scale on QKV / gate_up / LM
   head (a LazyNorm input), SwiGLU on gate_up: the skinny-M weight-streaming kernel (csrc/kernels/gemm_skinny.hip,
-  M <= 64: jump-forward forwards, tail decode buckets) and the ping-pong tile GEMM (csrc/kernels/gemm_pp.hip) above,
+  M <= 128: jump-forward forwards, tail decode buckets) and the ping-pong tile GEMM (csrc/kernels/gemm_pp.hip) above,
   with the kernel, tile config and split-K of the measured plan (``gemm_plan.json``: per (N, K, epilogue) the best
   by M range, from ``scripts/tune_gemm_pp.py`` on one MI355X, random operands, cold weights; plan cfg >= 100 is
   skinny config cfg - 100);
@@ -35,8 +35,8 @@ _PP_BN = {0: 256, 1: 256, 2: 128, 3: 128, 4: 256, 5: 256, 6: 128, 7: 128, 8: 256
 _PP_RATE = {0: 1.0, 1: 0.84, 2: 0.84, 3: 0.66, 4: 1.0, 5: 0.71, 6: 0.73, 7: 0.6, 8: 1.0, 9: 0.84, 10: 0.84, 11: 0.66}
 # skinny-M configs (gemm_skinny.hip SK_CONFIGS): plan id SK_BASE + c -> (RT: W tiles of 16 rows, MT: M <= 16 MT)
 SK_BASE = 100
-_SK = {0: (1, 1), 1: (2, 1), 2: (4, 1), 3: (2, 2), 4: (4, 2), 5: (2, 4), 6: (4, 4)}
-SKINNY_MAX_M = 64
+_SK = {0: (1, 1), 1: (2, 1), 2: (4, 1), 3: (2, 2), 4: (4, 2), 5: (2, 4), 6: (4, 4), 7: (2, 8)}
+SKINNY_MAX_M = 128
 _plan_cache: dict = {}
 _plan_table: Optional[dict] = None
 

@@ -35,7 +35,7 @@ def skinny_candidates(m, n, k, mode, keep=8):
 
     out = []
     for c, (rt, mt) in G._SK.items():
-        if m > 16 * mt or (mt > 1 and m <= 8 * mt and mt != 2):
+        if m > 16 * mt or (mt > 1 and m <= 8 * mt and mt not in (2, 8)):
             continue
         groups = (n // 2) // (8 * rt) if mode == 1 else n // (16 * rt)
         for sk in (1, 2, 3, 4, 7, 8, 14, 16):

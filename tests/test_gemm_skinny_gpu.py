@@ -11,7 +11,7 @@ pytestmark = pytest.mark.gpu
 
 DEV = "cuda"
 # cfg -> (RT, MT): csrc/kernels/gemm_skinny.hip SK_CONFIGS
-CFGS = {0: (1, 1), 1: (2, 1), 2: (4, 1), 3: (2, 2), 4: (4, 2), 5: (2, 4), 6: (4, 4)}
+CFGS = {0: (1, 1), 1: (2, 1), 2: (4, 1), 3: (2, 2), 4: (4, 2), 5: (2, 4), 6: (4, 4), 7: (2, 8)}
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -112,7 +112,7 @@ def test_decode_shapes_vs_library():
     """Llama-3-8B projection shapes at jump-forward / tail-bucket M against hipBLASLt, tight tolerance."""
     g = torch.Generator(device=DEV).manual_seed(1)
     for m, n, k, cfg, sk in [(4, 6144, 4096, 1, 1), (5, 4096, 14336, 2, 2), (32, 4096, 4096, 4, 4),
-                             (64, 28672, 4096, 6, 1), (16, 128256, 4096, 2, 1)]:
+                             (64, 28672, 4096, 6, 1), (16, 128256, 4096, 2, 1), (128, 4096, 14336, 7, 2)]:
         x = _rand((m, k), g)
         w = _rand((n, k), g, 0.05)
         y, _ = _sk(x, w, 0, cfg, sk)
