@@ -111,9 +111,10 @@ def quant_rows(x: torch.Tensor, resid: torch.Tensor | None = None, w: torch.Tens
     return ref.quant_rows(x, resid, w, eps, mode)
 
 
-# W8A8 GEMM routing, by measured shape (profiles/r1_fp8_gemm.json): the hand-written kernels where they win — the fp8
-# decode GEMV (M <= 4) and the MFMA GEMM with the fused SwiGLU epilogue for gate_up at M <= 128 — and hipBLASLt's fp8
-# GEMM with row-wise scales (torch._scaled_mm, a plain library GEMM) for the large tiles.  CHRONOS_QGEMM=own|lib|auto.
+# W8A8 GEMM routing, by measured shape: the "qplans" rows of ops/gemm_plan.json (scripts/tune_gemm_pp.py --fp8: the
+# hand-written fp8 GEMV / block-scaled MFMA GEMM against hipBLASLt's fp8 GEMM with row-wise scales, torch._scaled_mm,
+# per (N, K, SwiGLU) and M; the library only where it measured > 3 % faster).  Unmeasured shapes: the round-1 rule
+# (profiles/r1_fp8_gemm.json) — own GEMV at M <= 4, own SwiGLU GEMM at M <= 128.  CHRONOS_QGEMM=own|lib|auto.
 _QGEMM = os.environ.get("CHRONOS_QGEMM", "auto")
 _F8 = torch.float8_e4m3fn
 
@@ -121,6 +122,11 @@ _F8 = torch.float8_e4m3fn
 def _qown(m: int, n: int, k: int, swiglu: bool) -> bool:
     if _QGEMM != "auto":
         return _QGEMM == "own"
+    from .gemm import qplan_own
+
+    own = qplan_own(m, n, k, swiglu)  # the measured A/B of ops/gemm_plan.json "qplans"
+    if own is not None:
+        return own
     return (m <= 4 and k % 1024 == 0) or (swiglu and m <= 128)
 
 

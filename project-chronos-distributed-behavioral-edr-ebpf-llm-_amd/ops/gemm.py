@@ -39,10 +39,11 @@ _SK = {0: (1, 1), 1: (2, 1), 2: (4, 1), 3: (2, 2), 4: (4, 2), 5: (2, 4), 6: (4, 
 SKINNY_MAX_M = 128
 _plan_cache: dict = {}
 _plan_table: Optional[dict] = None
+_qplan_table: Optional[dict] = None
 
 
 def _plan_file() -> dict:
-    global _plan_table
+    global _plan_table, _qplan_table
     if _plan_table is None:
         import json
 
@@ -50,10 +51,24 @@ def _plan_file() -> dict:
         try:
             with open(path) as fh:
                 raw = json.load(fh)
-            _plan_table = {tuple(int(v) for v in key.split(",")): rows for key, rows in raw.get("plans", {}).items()}
         except FileNotFoundError:
-            _plan_table = {}
+            raw = {}
+        key = lambda k: tuple(int(v) for v in k.split(","))  # noqa: E731
+        _plan_table = {key(k): rows for k, rows in raw.get("plans", {}).items()}
+        _qplan_table = {key(k): rows for k, rows in raw.get("qplans", {}).items()}
     return _plan_table
+
+
+def qplan_own(m: int, n: int, k: int, swiglu: bool) -> Optional[bool]:
+    """W8A8 fp8 projection: True = the hand-written kernels (fp8.hip qgemv / block-scaled MFMA qgemm), False = the
+    library's fp8 GEMM, None = not measured.  Rows [measured M, 1 own / 0 library] per (N, K, swiglu) from
+    ``scripts/tune_gemm_pp.py --fp8``, read like the bf16 plan's."""
+    _plan_file()
+    rows = (_qplan_table or {}).get((n, k, int(swiglu)))
+    if not rows:
+        return None
+    pick = next((r for r in rows if m <= r[0]), rows[-1])
+    return bool(pick[1])
 
 
 def _sk_valid(c: int, m: int, n: int, k: int, mode: int, sk: int) -> bool:

@@ -23,20 +23,21 @@ def main():
     ap.add_argument("--jsonl", default="", help="merged table as JSON lines (for profiles/)")
     a = ap.parse_args()
 
-    merged, meta = {}, {}
+    merged, qmerged, meta = {}, {}, {}
     for path in a.plans:
         with open(path) as fh:
             raw = json.load(fh)
         meta = raw.get("meta", meta)
-        for key, rows in raw["plans"].items():
-            cur = {r[0]: r for r in merged.get(key, [])}
-            cur.update({r[0]: r for r in rows})
-            merged[key] = [cur[m] for m in sorted(cur)]
+        for dst, section in ((merged, "plans"), (qmerged, "qplans")):
+            for key, rows in raw.get(section, {}).items():
+                cur = {r[0]: r for r in dst.get(key, [])}
+                cur.update({r[0]: r for r in rows})
+                dst[key] = [cur[m] for m in sorted(cur)]
     if a.plans:
         meta = dict(meta, source="scripts/tune_gemm_pp.py on one MI355X (cold weights); merged by scripts/apply_tune.py")
         with open(a.out, "w") as fh:
-            json.dump({"meta": meta, "plans": merged}, fh, indent=1)
-        print(f"wrote {a.out}: {len(merged)} shapes")
+            json.dump({"meta": meta, "plans": merged, "qplans": qmerged}, fh, indent=1)
+        print(f"wrote {a.out}: {len(merged)} bf16 shapes, {len(qmerged)} fp8 shapes")
 
     recs = {}
     for path in a.tables:

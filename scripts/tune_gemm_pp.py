@@ -77,6 +77,7 @@ def main():
     ap.add_argument("--out-plan", default="")
     ap.add_argument("--out-table", default="")
     ap.add_argument("--merge", default="", help="plan file whose rows at M not measured in this run are kept")
+    ap.add_argument("--fp8", action="store_true", help="tune the W8A8 fp8 routing (qplans) instead of the bf16 plan")
     args = ap.parse_args()
     merged = {}
     if args.merge:
@@ -86,6 +87,8 @@ def main():
     from chronos.ops import gemm as G
 
     ops.load()
+    if args.fp8:
+        return tune_fp8(args, merged)
     dev = "cuda"
     ms = [int(v) for v in args.ms.split(",")]
     plans, table = {}, []
@@ -176,6 +179,75 @@ def main():
             fh.writelines(json.dumps(r) + "\n" for r in table)
     won = sum(r["route"] == "own" for r in table)
     print(f"hand-written kernel routed on {won}/{len(table)} (shape, M) points", flush=True)
+
+
+def tune_fp8(args, merged_unused):
+    """W8A8: the hand-written fp8 kernels (qgemv / block-scaled MFMA qgemm, fused SwiGLU) against hipBLASLt's fp8 GEMM
+    (+ silu_mul for gate_up), per 8B projection shape and M; rows [M, 1 own / 0 library] -> "qplans"."""
+    from chronos import ops
+
+    dev = "cuda"
+    ms = [int(v) for v in args.ms.split(",")]
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    qplans, table = {}, []
+    f8 = torch.float8_e4m3fn
+    for op, (n, k, mode) in SHAPES["8b"].items():
+        swiglu = mode == 1
+        g = torch.Generator(device=dev).manual_seed(0)
+        ncopy = max(2, -(-(600 << 20) // (n * k)))
+        wqs = [((torch.rand(n, k, device=dev, generator=g) * 2 - 1) * 200).to(f8).view(torch.uint8)
+               for _ in range(ncopy)]
+        wsc = torch.rand(n, device=dev, generator=g) * 1e-3 + 1e-4
+        rows = []
+        for m in ms:
+            if op == "lm_head":
+                continue  # the LM head stays bf16 in the W8A8 model
+            xq = ((torch.rand(m, k, device=dev, generator=g) * 2 - 1) * 200).to(f8).view(torch.uint8)
+            xs = torch.rand(m, device=dev, generator=g) * 1e-2 + 1e-3
+
+            def own(i):
+                return torch.ops.chronos.qlinear(xq, xs, wqs[i % ncopy], wsc, swiglu)
+
+            def lib(i):
+                y = ops._qlib(xq, xs, wqs[i % ncopy], wsc)
+                return ops.silu_mul(y) if swiglu else y
+
+            ref = lib(0).float()
+            err = (own(0).float() - ref).abs().max().item()
+            assert err <= 0.03 * (ref.abs().max().item() + 1e-6), f"fp8 {op} M={m}: err {err}"
+            flop = 2.0 * m * n * k
+            iters = max(2, min(args.iters, int(4e13 / flop) + 2))
+            t = {"own": [], "lib": []}
+            for _ in range(args.rounds):
+                for name, fn in (("lib", lib), ("own", own)):
+                    fn(0)
+                    torch.cuda.synchronize()
+                    st.record()
+                    for i in range(iters):
+                        fn(i)
+                    en.record()
+                    torch.cuda.synchronize()
+                    t[name].append(st.elapsed_time(en) * 1000 / iters)
+            own_us, lib_us = min(t["own"]), min(t["lib"])
+            use_own = not lib_us < own_us / 1.03
+            rows.append([m, int(use_own)])
+            rec = dict(model="8b-fp8", op=op, m=m, n=n, k=k, mode=mode, lib_us=round(lib_us, 2),
+                       own_us=round(own_us, 2), own="fp8.hip", lib_TF=round(flop / lib_us / 1e6, 1),
+                       own_TF=round(flop / own_us / 1e6, 1), own_weight_TBs=round(n * k / own_us / 1e6, 2),
+                       speedup=round(lib_us / own_us, 3), route="own" if use_own else "lib", all={})
+            table.append(rec)
+            print(json.dumps(rec), flush=True)
+        if rows:
+            qplans[f"{n},{k},{int(swiglu)}"] = rows
+        del wqs
+        torch.cuda.empty_cache()
+    if args.out_plan:
+        with open(args.out_plan, "w") as fh:
+            json.dump({"meta": {"device": torch.cuda.get_device_name(0), "note": "qplans rows: [measured M, own]"},
+                       "plans": {}, "qplans": qplans}, fh, indent=1)
+    if args.out_table:
+        with open(args.out_table, "w") as fh:
+            fh.writelines(json.dumps(r) + "\n" for r in table)
 
 
 if __name__ == "__main__":

@@ -60,3 +60,17 @@ def test_own_mode_uses_skinny_then_tiles(monkeypatch):
     monkeypatch.setattr(G, "PP_MODE", "own")
     assert G.pp_plan(5, 4096, 4096, G.PP_PLAIN)[0] >= G.SK_BASE
     assert G.pp_plan(512, 4096, 4096, G.PP_PLAIN)[0] < G.SK_BASE
+
+
+def test_fp8_qplan(monkeypatch):
+    monkeypatch.setattr(G, "_plan_table", {})
+    monkeypatch.setattr(G, "_qplan_table", {(28672, 4096, 1): [[4, 1], [128, 1], [1024, 0], [16384, 1]]})
+    assert G.qplan_own(3, 28672, 4096, True) is True
+    assert G.qplan_own(512, 28672, 4096, True) is False
+    assert G.qplan_own(20000, 28672, 4096, True) is True
+    assert G.qplan_own(5, 28672, 4096, False) is None
+    from chronos import ops
+
+    monkeypatch.setattr(ops, "_QGEMM", "auto")
+    assert ops._qown(512, 28672, 4096, True) is False
+    assert ops._qown(3, 4096, 4096, False) is True  # unmeasured: the round-1 rule (GEMV at M <= 4)
