@@ -28,10 +28,11 @@ bool launch_gemm_pp(int cfg, int mode, bool normp, bool prio, const PPArgs& a, h
 
 // skinny-M family (csrc/kernels/gemm_skinny.hip, M <= 16 * MT): same PPArgs / epilogues; the workgroup owns 16 * RT
 // W rows (swiglu: 8 * RT gate + 8 * RT up), ws holds [groups * splitk, 64 * RT * MT] f32x4 slabs, cnt one ticket per
-// group, kResid partials are [M, N / (16 * RT)]; K % (256 * splitk) == 0
-constexpr int kSkinnyConfigs = 8;
+// group, kResid partials are [M, N / (16 * RT)]; K % (64 * NW * splitk) == 0
+constexpr int kSkinnyConfigs = 12;
 int gemm_skinny_rt(int cfg);
 int gemm_skinny_mt(int cfg);
+int gemm_skinny_nw(int cfg);  // waves per workgroup
 bool launch_gemm_skinny(int cfg, int mode, bool normp, const PPArgs& a, hipStream_t st);
 
 }  // namespace chronos

@@ -558,9 +558,10 @@ std::tuple<Tensor, Tensor> gemm_skinny(const Tensor& x, const Tensor& w, int64_t
     CHK(cfg >= 0 && cfg < chronos::kSkinnyConfigs, "gemm_skinny: cfg");
     CHK(mode >= 0 && mode <= 2, "gemm_skinny: mode");
     const int RT = chronos::gemm_skinny_rt((int)cfg), MT = chronos::gemm_skinny_mt((int)cfg);
+    const int NW = chronos::gemm_skinny_nw((int)cfg);
     CHK(M >= 1 && M <= 16 * MT, "gemm_skinny: M must be in [1, 16 * MT] of the config");
-    CHK(splitk >= 1 && K % (256 * splitk) == 0 && K <= (1 << 20) && N * K < (1LL << 40),
-        "gemm_skinny: K % (256 * splitk) == 0");
+    CHK(splitk >= 1 && K % (64 * NW * splitk) == 0 && K <= (1 << 20) && N * K < (1LL << 40),
+        "gemm_skinny: K % (64 * NW * splitk) == 0");
     CHK(mode == 1 ? RT % 2 == 0 && (N / 2) % (8 * RT) == 0 && N % 2 == 0 : N % (16 * RT) == 0,
         "gemm_skinny: N % (16 RT) (swiglu: F % (8 RT), RT even)");
     CHK(mode != 2 || !part_in.has_value(), "gemm_skinny: resid mode has no norm prologue");

@@ -7,8 +7,11 @@
 //
 // At these M the op is a weight stream (the whole W once per call) with at most 64 columns of arithmetic per weight
 // element, so the design is the decode GEMV's (gemv.hip) with the dot products moved onto the matrix cores:
-//   * a workgroup owns 16*RT output rows (RT MFMA A tiles) and a K range; its 4 waves split that range in 64-k
-//     units (wave w takes units w, w+4, ...), so the main loop has no barrier and no LDS at all;
+//   * a workgroup owns 16*RT output rows (RT MFMA A tiles) and a K range; its NW waves split that range in 64-k
+//     units (wave w takes units w, w+NW, ...), so the main loop has no barrier and no LDS at all.  NW up to 16 waves
+//     gives the latency hiding of 4 waves per SIMD without splitting K across workgroups: a cross-workgroup split
+//     costs an agent-scope release per workgroup (an L2 write-back) plus the slab round trip — 15-25 us on the 8B
+//     decode shapes, more than the whole weight stream (profiles/r3_gemm_table.md);
 //   * W goes straight from HBM into VGPRs in the v_mfma_f32_16x16x32_bf16 A layout (lane l: row l&15, k 8(l>>4)..+8
 //     of each 32-k block).  A unit is two such loads per A tile, i.e. one full 128-B line of each of 16 rows;
 //     x (L2-resident: <= 128 x K bf16) comes the same way as the B operand (column = x row l&15), rows >= M clamped;
@@ -16,7 +19,7 @@
 //     counted waits retire the oldest unit only);
 //   * MT x tiles of 16 rows (M <= 16 MT), RT W tiles: x bytes / W bytes = MT / RT per wave, kept <= 2 so the TCP
 //     carries the weight stream plus the x re-reads;
-//   * the 4 waves' accumulators meet in LDS (fixed order), optional split-K across workgroups through fp32 slabs with
+//   * the NW waves' accumulators meet in LDS (fixed order), optional split-K across workgroups through fp32 slabs with
 //     an agent-scope ticket whose last arriver sums the slabs in slice order (bitwise reproducible, graph == eager);
 //   * epilogue per (row m, 4 consecutive outputs): 8-byte stores, CPR consecutive lanes cover a row's 16 RT outputs.
 #include "chronos_gemm.h"
@@ -27,19 +30,20 @@ namespace {
 
 enum : int { kPlain = kPPPlain, kSwiglu = kPPSwiglu, kResid = kPPResid };
 
-template <int RT, int MT, int D, int MODE, bool NORMP>
-__global__ void __launch_bounds__(256) skinny_kernel(PPArgs a) {
+template <int RT, int MT, int D, int NW, int MODE, bool NORMP>
+__global__ void __launch_bounds__(64 * NW) skinny_kernel(PPArgs a) {
     static_assert(MODE != kSwiglu || RT % 2 == 0, "swiglu: RT/2 gate tiles + RT/2 up tiles");
+    constexpr int NT = 64 * NW;                        // threads
     constexpr int UNITS = RT * MT * 64;                // f32x4 accumulators per wave
     constexpr int CPR = MODE == kSwiglu ? 2 * RT : 4 * RT;  // output units (4 columns each) per row
     constexpr int NOUT = 16 * MT * CPR;                // output units per workgroup (a multiple of 64)
-    constexpr int VP = NOUT >= 256 ? NOUT / 256 : 1;   // output units per thread
+    constexpr int VP = NOUT >= NT ? NOUT / NT : 1;     // output units per thread
     constexpr int PAIR = MODE == kSwiglu ? 2 : 1;       // swiglu: a gate unit and its up unit
     constexpr int NP = NOUT + NOUT / 16;               // one padded half (pad: 1 slot per 16, see red_at)
     constexpr int SZ = PAIR * NP;                      // f32x4 slots per wave
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    f32x4* red = reinterpret_cast<f32x4*>(smem);       // [4 waves][SZ]
-    float* inv = reinterpret_cast<float*>(smem + 4 * SZ * 16);  // [16 MT]
+    f32x4* red = reinterpret_cast<f32x4*>(smem);       // [NW waves][SZ]
+    float* inv = reinterpret_cast<float*>(smem + NW * SZ * 16);  // [16 MT]
     int* flag = reinterpret_cast<int*>(inv + 16 * MT);
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -48,7 +52,7 @@ __global__ void __launch_bounds__(256) skinny_kernel(PPArgs a) {
     const int task = xcd_remap(blockIdx.x, G * S);
     const int g = task / S, s = task - g * S;
     const int KS = K / S;
-    const int NU = KS >> 8;  // 64-k units per wave
+    const int NU = KS / (64 * NW);  // 64-k units per wave
     const int kbase = s * KS + wave * 64 + 8 * (lane >> 4);
 
     const bf16x8* wp[RT];
@@ -66,10 +70,10 @@ __global__ void __launch_bounds__(256) skinny_kernel(PPArgs a) {
     for (int mt = 0; mt < MT; ++mt)
         xp[mt] = reinterpret_cast<const bf16x8*>(a.x + (int64_t)min(16 * mt + (lane & 15), M - 1) * K + kbase);
 
-    // unit u of this wave covers k = kbase + 256 u + {0, 32} (+ 8 (lane >> 4) already in the pointers)
+    // unit u of this wave covers k = kbase + 64 NW u + {0, 32} (+ 8 (lane >> 4) already in the pointers)
     bf16x8 wr[D][RT][2], xr[D][MT][2];
     auto load = [&](int u, int d) {
-        const int off = u * 32;  // 256 bf16 = 32 bf16x8
+        const int off = u * 8 * NW;  // 64 NW bf16 = 8 NW bf16x8
 #pragma unroll
         for (int rt = 0; rt < RT; ++rt) {
             wr[d][rt][0] = __builtin_nontemporal_load(wp[rt] + off);
@@ -112,7 +116,7 @@ __global__ void __launch_bounds__(256) skinny_kernel(PPArgs a) {
     // NORMP: inv[m] of the x rows from the producer's partials — fetched only now, so these loads never sit in front
     // of the weight ring in the in-order vmcnt queue
     if constexpr (NORMP) {
-        for (int r = wave; r < 16 * MT; r += 4) {
+        for (int r = wave; r < 16 * MT; r += NW) {
             const int m = min(r, M - 1);
             float ss = 0.f;
             for (int i = lane; i < a.nparts_in; i += 64) ss += a.part_in[(int64_t)m * a.nparts_in + i];
@@ -142,9 +146,11 @@ __global__ void __launch_bounds__(256) skinny_kernel(PPArgs a) {
         for (int j = 0; j < VP; ++j)
 #pragma unroll
             for (int p = 0; p < PAIR; ++p) {
-                const int v = tid + 256 * j;
-                val[j][p] = ((red[red_at(0, p, v)] + red[red_at(1, p, v)]) + red[red_at(2, p, v)]) +
-                            red[red_at(3, p, v)];
+                const int v = tid + NT * j;
+                f32x4 acc4 = red[red_at(0, p, v)];
+#pragma unroll
+                for (int w = 1; w < NW; ++w) acc4 += red[red_at(w, p, v)];
+                val[j][p] = acc4;
             }
     }
 
@@ -155,7 +161,7 @@ __global__ void __launch_bounds__(256) skinny_kernel(PPArgs a) {
 #pragma unroll
             for (int j = 0; j < VP; ++j)
 #pragma unroll
-                for (int p = 0; p < PAIR; ++p) slab[(tid + 256 * j) * PAIR + p] = val[j][p];
+                for (int p = 0; p < PAIR; ++p) slab[(tid + NT * j) * PAIR + p] = val[j][p];
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
@@ -180,7 +186,7 @@ __global__ void __launch_bounds__(256) skinny_kernel(PPArgs a) {
                 for (int j = 0; j < VP; ++j)
 #pragma unroll
                     for (int p = 0; p < PAIR; ++p) {
-                        const f32x4 v = base[(int64_t)o * SLAB + (tid + 256 * j) * PAIR + p];
+                        const f32x4 v = base[(int64_t)o * SLAB + (tid + NT * j) * PAIR + p];
                         val[j][p] = o == 0 ? v : val[j][p] + v;
                     }
             }
@@ -190,7 +196,7 @@ __global__ void __launch_bounds__(256) skinny_kernel(PPArgs a) {
 
 #pragma unroll
     for (int j = 0; j < VP; ++j) {
-        const int v = tid + 256 * j;
+        const int v = tid + NT * j;
         const int r = v / CPR, c = v % CPR;
         const bool live = r < M;
         float sc = 1.f;
@@ -235,39 +241,44 @@ __global__ void __launch_bounds__(256) skinny_kernel(PPArgs a) {
     }
 }
 
-template <int RT, int MT, int D, int MODE, bool NORMP>
+template <int RT, int MT, int D, int NW, int MODE, bool NORMP>
 void launch_cfg(const PPArgs& a, hipStream_t st) {
     constexpr int UNITS = RT * MT * 64;
-    const int lds = 4 * (UNITS + UNITS / 16) * 16 + 16 * MT * 4 + 16;
-    auto kern = skinny_kernel<RT, MT, D, MODE, NORMP>;
+    const int lds = NW * (UNITS + UNITS / 16) * 16 + 16 * MT * 4 + 16;
+    auto kern = skinny_kernel<RT, MT, D, NW, MODE, NORMP>;
     static bool attr = false;
     if (!attr) {
         hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         attr = true;
     }
     const int G = MODE == kSwiglu ? a.F / (8 * RT) : a.N / (16 * RT);
-    hipLaunchKernelGGL(kern, dim3(G * a.splitk), dim3(256), lds, st, a);
+    hipLaunchKernelGGL(kern, dim3(G * a.splitk), dim3(64 * NW), lds, st, a);
 }
 
-// configs {RT (W tiles of 16 rows per workgroup), MT (x tiles: M <= 16 MT), D (ring depth in 64-k units)}
-#define SK_CONFIGS(X) \
-    X(0, 1, 1, 8)     \
-    X(1, 2, 1, 6)     \
-    X(2, 4, 1, 4)     \
-    X(3, 2, 2, 4)     \
-    X(4, 4, 2, 3)     \
-    X(5, 2, 4, 3)     \
-    X(6, 4, 4, 2)     \
-    X(7, 2, 8, 2)
+// configs {RT (W tiles of 16 rows per workgroup), MT (x tiles: M <= 16 MT), D (ring depth in 64-k units), NW (waves
+// splitting K inside the workgroup; K % (64 NW splitk) == 0)}
+#define SK_CONFIGS(X)  \
+    X(0, 1, 1, 4, 16)  \
+    X(1, 2, 1, 4, 8)   \
+    X(2, 4, 1, 4, 4)   \
+    X(3, 2, 2, 4, 8)   \
+    X(4, 4, 2, 3, 4)   \
+    X(5, 2, 4, 3, 4)   \
+    X(6, 4, 4, 2, 4)   \
+    X(7, 2, 8, 2, 4)   \
+    X(8, 1, 2, 4, 16)  \
+    X(9, 1, 4, 2, 16)  \
+    X(10, 2, 4, 2, 8)  \
+    X(11, 1, 1, 4, 8)
 
 template <int MODE, bool NORMP>
 bool launch_mode(int cfg, const PPArgs& a, hipStream_t st) {
     switch (cfg) {
-#define SK_CASE(ID, RT_, MT_, D_)                                          \
+#define SK_CASE(ID, RT_, MT_, D_, NW_)                                     \
     case ID:                                                               \
         if constexpr (MODE == kSwiglu && RT_ % 2) return false;            \
         else {                                                             \
-            launch_cfg<RT_, MT_, D_, MODE, NORMP>(a, st);                  \
+            launch_cfg<RT_, MT_, D_, NW_, MODE, NORMP>(a, st);             \
             return true;                                                   \
         }
         SK_CONFIGS(SK_CASE)
@@ -280,15 +291,23 @@ bool launch_mode(int cfg, const PPArgs& a, hipStream_t st) {
 
 int gemm_skinny_rt(int cfg) {
     switch (cfg) {
-#define SK_RT(ID, RT_, MT_, D_) case ID: return RT_;
+#define SK_RT(ID, RT_, MT_, D_, NW_) case ID: return RT_;
         SK_CONFIGS(SK_RT)
 #undef SK_RT
         default: return 0;
     }
 }
+int gemm_skinny_nw(int cfg) {
+    switch (cfg) {
+#define SK_NW(ID, RT_, MT_, D_, NW_) case ID: return NW_;
+        SK_CONFIGS(SK_NW)
+#undef SK_NW
+        default: return 0;
+    }
+}
 int gemm_skinny_mt(int cfg) {
     switch (cfg) {
-#define SK_MT(ID, RT_, MT_, D_) case ID: return MT_;
+#define SK_MT(ID, RT_, MT_, D_, NW_) case ID: return MT_;
         SK_CONFIGS(SK_MT)
 #undef SK_MT
         default: return 0;

@@ -24,7 +24,9 @@ from typing import Callable, Optional
 import torch
 
 # Largest M routed to the GEMV (gemv_ok).  Env CHRONOS_GEMV_MAX_M; scripts/single_stream.py A/Bs it (py_gemv_max_m).
-GEMV_MAX_M = int(os.environ.get("CHRONOS_GEMV_MAX_M", "2"))
+# M = 2 goes to the skinny MFMA GEMM: the two-row GEMV streams at 1-3.5 TB/s against 4-5.5 at M = 1 and the skinny
+# kernel's 3.4-4.9 at M = 3 (profiles/r3_gemm_table.md).
+GEMV_MAX_M = int(os.environ.get("CHRONOS_GEMV_MAX_M", "1"))
 
 # ---- the batched GEMM family (gemm_pp.hip) ----------------------------------------------------------------------
 PP_MODE = os.environ.get("CHRONOS_PP", "auto")  # auto | own | lib
@@ -33,9 +35,11 @@ _PP_BM = {0: 256, 1: 128, 2: 256, 3: 128, 4: 256, 5: 128, 6: 256, 7: 128, 8: 256
 _PP_BN = {0: 256, 1: 256, 2: 128, 3: 128, 4: 256, 5: 256, 6: 128, 7: 128, 8: 256, 9: 256, 10: 128, 11: 128}
 # relative per-CU MAC rate of each tile config at full occupancy (gate_up M = 1024 sweep, profiles/r3_gemm_pp_*)
 _PP_RATE = {0: 1.0, 1: 0.84, 2: 0.84, 3: 0.66, 4: 1.0, 5: 0.71, 6: 0.73, 7: 0.6, 8: 1.0, 9: 0.84, 10: 0.84, 11: 0.66}
-# skinny-M configs (gemm_skinny.hip SK_CONFIGS): plan id SK_BASE + c -> (RT: W tiles of 16 rows, MT: M <= 16 MT)
+# skinny-M configs (gemm_skinny.hip SK_CONFIGS): plan id SK_BASE + c -> (RT: W tiles of 16 rows, MT: M <= 16 MT,
+# NW: waves splitting K inside the workgroup)
 SK_BASE = 100
-_SK = {0: (1, 1), 1: (2, 1), 2: (4, 1), 3: (2, 2), 4: (4, 2), 5: (2, 4), 6: (4, 4), 7: (2, 8)}
+_SK = {0: (1, 1, 16), 1: (2, 1, 8), 2: (4, 1, 4), 3: (2, 2, 8), 4: (4, 2, 4), 5: (2, 4, 4), 6: (4, 4, 4),
+       7: (2, 8, 4), 8: (1, 2, 16), 9: (1, 4, 16), 10: (2, 4, 8), 11: (1, 1, 8)}
 SKINNY_MAX_M = 128
 _plan_cache: dict = {}
 _plan_table: Optional[dict] = None
@@ -72,8 +76,8 @@ def qplan_own(m: int, n: int, k: int, swiglu: bool) -> Optional[bool]:
 
 
 def _sk_valid(c: int, m: int, n: int, k: int, mode: int, sk: int) -> bool:
-    rt, mt = _SK[c]
-    if m > 16 * mt or k % (256 * sk):
+    rt, mt, nw = _SK[c]
+    if m > 16 * mt or k % (64 * nw * sk):
         return False
     return (rt % 2 == 0 and n % 2 == 0 and (n // 2) % (8 * rt) == 0) if mode == PP_SWIGLU else n % (16 * rt) == 0
 
@@ -82,14 +86,16 @@ def _sk_model(m: int, n: int, k: int, mode: int, cus: int = 256) -> Optional[tup
     """Cost-model pick of a skinny config: the narrowest x tile covering M, W tiles >= x tiles (x re-read bytes <=
     weight bytes), split-K until the grid covers the CUs twice."""
     best = None
-    for c, (rt, mt) in _SK.items():
+    for c, (rt, mt, nw) in _SK.items():
         if m > 16 * mt or (mt > 1 and m <= 8 * mt):
             continue
         groups = (n // 2) // (8 * rt) if mode == PP_SWIGLU else n // (16 * rt)
         for sk in (1, 2, 4, 7, 8, 14, 16):
             if not _sk_valid(c, m, n, k, mode, sk):
                 continue
-            t = (rt < mt, -min(groups * sk, 2 * cus), sk, -rt)
+            # a cross-workgroup split costs more than it hides (profiles/r3_gemm_table.md): only when the grid
+            # would otherwise leave CUs idle; then the widest workgroups
+            t = (sk > 1 and groups >= cus, rt < mt, -min(groups * sk, cus), sk, -nw, -rt)
             if best is None or t < best[0]:
                 best = (t, (SK_BASE + c, sk))
     return best[1] if best else None
@@ -124,7 +130,7 @@ def _pp_model(m: int, n: int, k: int, mode: int, cus: int = 256) -> tuple[int, i
 def pp_plan(m: int, n: int, k: int, mode: int = PP_PLAIN) -> Optional[tuple[int, int]]:
     """(config, split-K) of the hand-written batched GEMM for this shape — config >= SK_BASE is the skinny kernel —
     or None for the library."""
-    if m < 3 or PP_MODE == "lib":
+    if m <= GEMV_MAX_M or PP_MODE == "lib":
         return None
     key = (m, n, k, mode)
     hit = _plan_cache.get(key, False)
@@ -218,7 +224,7 @@ def gemv_resid(x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor) -> ResidOu
     from . import _k
 
     m, k = x.numel() // x.shape[-1], x.shape[-1]
-    if m > 2:
+    if m > GEMV_MAX_M:
         s, part = pp_gemm(x, w, PP_RESID, pp_plan(m, w.shape[0], k, PP_RESID), resid.reshape(m, -1))
         return ResidOut(s.view(resid.shape), part)
     s = torch.empty(resid.shape, dtype=resid.dtype, device=resid.device)
@@ -229,14 +235,14 @@ def gemv_resid(x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor) -> ResidOu
 def resid_ok(m: int, n: int, k: int) -> bool:
     """Shapes of the residual-epilogue producer: the M <= 2 GEMV shapes (gemv.hip kResid) and the batched GEMM's
     (gemm_pp.hip kResid) where the plan takes it."""
-    if m <= 2:
+    if m <= GEMV_MAX_M:
         return gemv_ok(m, n, k)
     return pp_plan(m, n, k, PP_RESID) is not None
 
 
 def gemv_ok(m: int, n: int, k: int, swiglu: bool = False) -> bool:
-    """Shapes routed to the hand-written decode GEMV (csrc/kernels/gemv.hip): K % 512, N % 16 and the M range where it
-    beats hipBLASLt on cold weights (profiles/r1_kernels.json): M == 1 always, M == 2 below LM-head widths."""
+    """Shapes routed to the hand-written decode GEMV (csrc/kernels/gemv.hip): K % 512, N % 16, M <= GEMV_MAX_M (1 by
+    default; M = 2 only below LM-head widths when raised)."""
     if k % 512 or n % 16:
         return False
     return m == 1 or (m <= GEMV_MAX_M and n <= 32768)

@@ -30,19 +30,21 @@ SHAPES = {
 MS = [1, 2, 3, 4, 5, 8, 16, 32, 48, 64, 128, 256, 512, 768, 1024, 2048, 4096, 8192, 16384]
 
 
-def skinny_candidates(m, n, k, mode, keep=8):
+def skinny_candidates(m, n, k, mode, keep=10):
+    """Skinny configs whose x tile covers M: every valid one without split-K, plus splits only while the grid is
+    below two workgroups per CU (a split costs an L2 write-back per workgroup)."""
     from chronos.ops import gemm as G
 
     out = []
-    for c, (rt, mt) in G._SK.items():
+    for c, (rt, mt, nw) in G._SK.items():
         if m > 16 * mt or (mt > 1 and m <= 8 * mt and mt not in (2, 8)):
             continue
         groups = (n // 2) // (8 * rt) if mode == 1 else n // (16 * rt)
-        for sk in (1, 2, 3, 4, 7, 8, 14, 16):
-            if G._sk_valid(c, m, n, k, mode, sk) and 192 <= groups * sk <= 4096 and (sk == 1 or groups < 1024):
-                out.append((groups * sk, G.SK_BASE + c, sk))
-    out.sort(key=lambda t: abs(t[0] - 768))
-    return [(c, sk) for _, c, sk in out[:keep]]
+        for sk in (1, 2, 3, 4, 7, 8):
+            if G._sk_valid(c, m, n, k, mode, sk) and (sk == 1 or groups * sk <= 512):
+                out.append((sk > 1, -nw, G.SK_BASE + c, sk))
+    out.sort()
+    return [(c, sk) for _, _, c, sk in out[:keep]]
 
 
 def candidates(m, n, k, mode, keep=6):
@@ -120,7 +122,7 @@ def main():
                                                              None, 1e-5)[0]
                     return torch.ops.chronos.gemm_pp(x, ws[i % ncopy], mode, c[0], c[1], resid, None, 1e-5, False)[0]
 
-                if m <= 2:
+                if m == 1:
                     if not G.gemv_ok(m, n, k):
                         continue
                     cands = [("gemv", 1)]
@@ -148,14 +150,14 @@ def main():
                 best = min(cands, key=lambda c: min(times[c]))
                 lib_us, own_us = min(times["lib"]), min(times[best])
                 use_lib = lib_us < own_us / 1.03
-                if m > 2:
+                if m > 1:
                     rows.append([m, -1 if use_lib else best[0], 1 if use_lib else best[1]])
                 wbytes = n * k * 2
                 rec = dict(model=model, op=op, m=m, n=n, k=k, mode=mode, lib_us=round(lib_us, 2),
                            own_us=round(own_us, 2), own=f"cfg{best[0]}_sk{best[1]}",
                            lib_TF=round(flop / lib_us / 1e6, 1), own_TF=round(flop / own_us / 1e6, 1),
                            own_weight_TBs=round(wbytes / own_us / 1e6, 2), lib_weight_TBs=round(wbytes / lib_us / 1e6, 2),
-                           speedup=round(lib_us / own_us, 3), route="lib" if use_lib and m > 2 else "own",
+                           speedup=round(lib_us / own_us, 3), route="lib" if use_lib and m > 1 else "own",
                            all={f"cfg{c[0]}_sk{c[1]}": round(min(times[c]), 2) for c in cands})
                 table.append(rec)
                 print(json.dumps(rec), flush=True)

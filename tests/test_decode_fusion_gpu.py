@@ -24,6 +24,15 @@ def _lib():
     assert "_C" in n._loaded, "HIP kernel library must be the one running"
 
 
+@pytest.fixture(autouse=True)
+def _two_row_gemv(monkeypatch):
+    """These tests pin the GEMV kernels at M = 1 and 2; the engine routes M = 2 to the skinny GEMM by default
+    (ops/gemm.py GEMV_MAX_M), so the two-row GEMV variants are exercised here explicitly."""
+    from chronos.ops import gemm
+
+    monkeypatch.setattr(gemm, "GEMV_MAX_M", 2)
+
+
 @pytest.fixture(params=[0, 37], ids=["grid", "persist37"])
 def persist(request):
     """gemv.hip knob gemv_persist: 0 = one workgroup per row group; 37 = a 37-workgroup grid looping over the groups

@@ -9,7 +9,7 @@ from chronos.ops import gemm as G
 @pytest.fixture
 def plan(monkeypatch):
     table = {(4096, 4096, 2): [[5, 101, 2], [64, 106, 8], [256, 1, 2], [1024, -1, 1], [4096, 0, 1]],
-             (6144, 4096, 0): [[8, 100, 3]]}  # split 3 does not divide 4096 / 256: invalid -> library
+             (6144, 4096, 0): [[8, 100, 3]]}  # split 3 does not divide 4096 / 1024: invalid -> library
     monkeypatch.setattr(G, "_plan_table", table)
     monkeypatch.setattr(G, "_plan_cache", {})
     monkeypatch.setattr(G, "PP_MODE", "auto")
@@ -17,7 +17,8 @@ def plan(monkeypatch):
 
 
 def test_plan_rows_by_m(plan):
-    assert G.pp_plan(2, 4096, 4096, G.PP_RESID) is None  # M <= 2: the GEMV, never the plan
+    assert G.pp_plan(1, 4096, 4096, G.PP_RESID) is None  # M = 1: the GEMV, never the plan
+    assert G.pp_plan(2, 4096, 4096, G.PP_RESID) == (101, 2)  # M = 2: the first row
     assert G.pp_plan(3, 4096, 4096, G.PP_RESID) == (101, 2)
     assert G.pp_plan(5, 4096, 4096, G.PP_RESID) == (101, 2)
     assert G.pp_plan(6, 4096, 4096, G.PP_RESID) == (106, 8)
@@ -47,8 +48,8 @@ def test_skinny_model_valid(m, n, k, mode):
     if got is None:
         return
     cfg, sk = got
-    rt, mt = G._SK[cfg - G.SK_BASE]
-    assert m <= 16 * mt and k % (256 * sk) == 0
+    rt, mt, nw = G._SK[cfg - G.SK_BASE]
+    assert m <= 16 * mt and k % (64 * nw * sk) == 0
     if mode == G.PP_SWIGLU:
         assert rt % 2 == 0 and (n // 2) % (8 * rt) == 0
     else:

@@ -10,8 +10,9 @@ import torch
 pytestmark = pytest.mark.gpu
 
 DEV = "cuda"
-# cfg -> (RT, MT): csrc/kernels/gemm_skinny.hip SK_CONFIGS
-CFGS = {0: (1, 1), 1: (2, 1), 2: (4, 1), 3: (2, 2), 4: (4, 2), 5: (2, 4), 6: (4, 4), 7: (2, 8)}
+# cfg -> (RT, MT, NW): csrc/kernels/gemm_skinny.hip SK_CONFIGS
+CFGS = {0: (1, 1, 16), 1: (2, 1, 8), 2: (4, 1, 4), 3: (2, 2, 8), 4: (4, 2, 4), 5: (2, 4, 4), 6: (4, 4, 4),
+        7: (2, 8, 4), 8: (1, 2, 16), 9: (1, 4, 16), 10: (2, 4, 8), 11: (1, 1, 8)}
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -41,9 +42,9 @@ def _check(y, ref, tol=2e-2):
 @pytest.mark.parametrize("cfg", sorted(CFGS))
 @pytest.mark.parametrize("splitk", [1, 2, 3])
 def test_plain(cfg, splitk):
-    rt, mt = CFGS[cfg]
+    rt, mt, nw = CFGS[cfg]
     g = torch.Generator(device=DEV).manual_seed(7 * cfg + splitk)
-    n, k = 64 * 12, 256 * 6
+    n, k = 64 * 12, 64 * nw * splitk * 3
     for m in sorted({1, 3, 16 * mt - 5, 16 * mt}):
         x = _rand((m, k), g, 1.0, 0.1)
         w = _rand((n, k), g, 0.5)
@@ -55,9 +56,9 @@ def test_plain(cfg, splitk):
 def test_splitk_deterministic(cfg):
     """Split-K sums the slabs in slice order: repeated calls are bitwise equal (a replayed graph == the eager step),
     and the tickets are left at zero by every call."""
-    rt, mt = CFGS[cfg]
+    rt, mt, nw = CFGS[cfg]
     g = torch.Generator(device=DEV).manual_seed(40 + cfg)
-    m, n, k = 16 * mt - 1, 512, 256 * 8
+    m, n, k = 16 * mt - 1, 512, 64 * nw * 8
     x = _rand((m, k), g)
     w = _rand((n, k), g, 0.5, 0.05)
     first, _ = _sk(x, w, 0, cfg, 8)
@@ -72,9 +73,9 @@ def test_splitk_deterministic(cfg):
 @pytest.mark.parametrize("cfg", [c for c in sorted(CFGS) if CFGS[c][0] % 2 == 0])
 @pytest.mark.parametrize("splitk", [1, 2])
 def test_swiglu_normp(cfg, splitk):
-    rt, mt = CFGS[cfg]
+    rt, mt, nw = CFGS[cfg]
     g = torch.Generator(device=DEV).manual_seed(3 + cfg)
-    m, f, k = 16 * mt - 3, 256, 512
+    m, f, k = 16 * mt - 3, 256, 64 * nw * 2
     s = _rand((m, k), g, 2.0, 0.3)
     w = _rand((2 * f, k), g, 0.3)
     sf = s.float()
@@ -94,9 +95,9 @@ def test_swiglu_normp(cfg, splitk):
 @pytest.mark.parametrize("cfg", sorted(CFGS))
 @pytest.mark.parametrize("splitk", [1, 4])
 def test_resid_partials(cfg, splitk):
-    rt, mt = CFGS[cfg]
+    rt, mt, nw = CFGS[cfg]
     g = torch.Generator(device=DEV).manual_seed(5 + cfg)
-    m, n, k = 16 * mt - 2, 512, 1024
+    m, n, k = 16 * mt - 2, 512, 64 * nw * 4
     x = _rand((m, k), g)
     w = _rand((n, k), g, 0.2)
     r = _rand((m, n), g, 4.0)
@@ -112,7 +113,9 @@ def test_decode_shapes_vs_library():
     """Llama-3-8B projection shapes at jump-forward / tail-bucket M against hipBLASLt, tight tolerance."""
     g = torch.Generator(device=DEV).manual_seed(1)
     for m, n, k, cfg, sk in [(4, 6144, 4096, 1, 1), (5, 4096, 14336, 2, 2), (32, 4096, 4096, 4, 4),
-                             (64, 28672, 4096, 6, 1), (16, 128256, 4096, 2, 1), (128, 4096, 14336, 7, 2)]:
+                             (64, 28672, 4096, 6, 1), (16, 128256, 4096, 2, 1), (128, 4096, 14336, 7, 2),
+                             (3, 4096, 14336, 0, 1), (30, 6144, 4096, 8, 1), (60, 4096, 4096, 9, 1),
+                             (3, 8192, 3584, 11, 1)]:
         x = _rand((m, k), g)
         w = _rand((n, k), g, 0.05)
         y, _ = _sk(x, w, 0, cfg, sk)
@@ -128,6 +131,6 @@ def test_rejects_bad_shapes():
     with pytest.raises(RuntimeError):
         _sk(x, w, 0, 0, 1)  # M = 20 > 16 MT for cfg 0
     with pytest.raises(RuntimeError):
-        _sk(x[:8], w, 0, 0, 3)  # K % (256 * 3)
+        _sk(x[:8], w, 0, 0, 1)  # K % (64 * 16)
     with pytest.raises(RuntimeError):
         _sk(x[:8], w, 1, 0, 1)  # swiglu needs RT even
