@@ -60,6 +60,8 @@ def parse():
     ap.add_argument("--async-harvest", action="store_true")
     ap.add_argument("--prefill-ramp", type=int, default=2048, help="first prefill step after idle (0 = full chunks)")
     ap.add_argument("--no-jump-forward", action="store_true", help="decode grammar-forced runs token by token")
+    ap.add_argument("--no-mixed", action="store_true",
+                    help="separate prefill steps (no prefill chunks riding in the decode batch's forward)")
     ap.add_argument("--mode", choices=["wave", "closed"], default="wave")
     ap.add_argument("--closed-steps", type=int, default=2,
                     help="wave mode: afterwards also time this many closed-loop steps (steady-state arrivals) and "
@@ -189,6 +191,7 @@ def main():
                        prefix_cache=not a.no_prefix_cache, partial_prefix=not a.no_partial_prefix,
                        async_harvest=a.async_harvest, seed=0,
                        prefill_ramp=a.prefill_ramp, jump_forward=not a.no_jump_forward,
+                       mixed_batching=not a.no_mixed,
                        weight_dtype=a.weights, tp_sequence_parallel=a.sequence_parallel)
     # TP: the ranks of a replica submit the same chains in the same order and step the same deterministic scheduler,
     # so they stay in lockstep by construction (the serving path adds the leader broadcast of parallel/tp_engine.py)
