@@ -184,6 +184,19 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(PPArgs a) {
 #pragma unroll
         for (int t = 0; t < MT; ++t) acc[s][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    // NORMP: the producer's partials of this wave's x rows, ALL loads issued before the DMA prologue (they are the
+    // oldest entries of the in-order vmcnt queue, so the reduction below waits for them alone, and one HBM latency
+    // covers every row — a row-by-row load -> wave_sum loop cost BM/8 serial latencies, 50 us per gate_up tile)
+    constexpr int RPW = BM / 8;  // x rows per wave
+    float pv[NORMP ? RPW : 1];
+    if constexpr (NORMP) {
+#pragma unroll
+        for (int j = 0; j < RPW; ++j) {
+            const int m = min(m0 + wave + 8 * j, M - 1);
+            pv[j] = lane < a.nparts_in ? a.part_in[(int64_t)m * a.nparts_in + lane] : 0.f;
+        }
+    }
+
     // ---- prologue: stages 0 .. STAGES-2 in flight (SPLIT: W chunks 0 .. DW-2 by group 0, x 0 .. DX-2 by group 1)
     if constexpr (SPLIT) {
         if (g == 0) {
@@ -202,14 +215,20 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(PPArgs a) {
     }
 
     if constexpr (NORMP) {
-        // inv[r] of the tile's x rows from the producer's partials, while the first stages are in flight
+        // inv[r] of the tile's x rows, while the first stages are in flight (producers with > 64 partials per row
+        // add the rest here, rare: only the M = 1 GEMV producer has more)
         float* inv = reinterpret_cast<float*>(smem + EXTRA + 16);
-        for (int r = wave; r < BM; r += 8) {
-            const int m = min(m0 + r, M - 1);
-            float ss = 0.f;
-            for (int i = lane; i < a.nparts_in; i += 64) ss += a.part_in[(int64_t)m * a.nparts_in + i];
-            ss = wave_sum(ss);
-            if (lane == 0) inv[r] = rsqrtf(ss / (float)K + a.eps);
+        if (a.nparts_in > 64) {
+#pragma unroll
+            for (int j = 0; j < RPW; ++j) {
+                const int m = min(m0 + wave + 8 * j, M - 1);
+                for (int i = lane + 64; i < a.nparts_in; i += 64) pv[j] += a.part_in[(int64_t)m * a.nparts_in + i];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < RPW; ++j) {
+            const float ss = wave_sum(pv[j]);
+            if (lane == 0) inv[wave + 8 * j] = rsqrtf(ss / (float)K + a.eps);
         }
     }
     if constexpr (SPLIT) {

@@ -116,12 +116,26 @@ __global__ void __launch_bounds__(64 * NW) skinny_kernel(PPArgs a) {
     // NORMP: inv[m] of the x rows from the producer's partials — fetched only now, so these loads never sit in front
     // of the weight ring in the in-order vmcnt queue
     if constexpr (NORMP) {
-        for (int r = wave; r < 16 * MT; r += NW) {
-            const int m = min(r, M - 1);
-            float ss = 0.f;
-            for (int i = lane; i < a.nparts_in; i += 64) ss += a.part_in[(int64_t)m * a.nparts_in + i];
-            ss = wave_sum(ss);
-            if (lane == 0) inv[r] = rsqrtf(ss / (float)K + a.eps);
+        // every load of the wave's rows issued before any is reduced: one memory latency, not one per row
+        constexpr int RPW = (16 * MT + NW - 1) / NW;
+        float pv[RPW];
+#pragma unroll
+        for (int j = 0; j < RPW; ++j) {
+            const int m = min(wave + NW * j, M - 1);
+            pv[j] = lane < a.nparts_in ? a.part_in[(int64_t)m * a.nparts_in + lane] : 0.f;
+        }
+        if (a.nparts_in > 64) {
+#pragma unroll
+            for (int j = 0; j < RPW; ++j) {
+                const int m = min(wave + NW * j, M - 1);
+                for (int i = lane + 64; i < a.nparts_in; i += 64) pv[j] += a.part_in[(int64_t)m * a.nparts_in + i];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < RPW; ++j) {
+            const int r = wave + NW * j;
+            const float ss = wave_sum(pv[j]);
+            if (lane == 0 && r < 16 * MT) inv[r] = rsqrtf(ss / (float)K + a.eps);
         }
     }
     // Output unit v = r * CPR + c: row r, outputs 4c..4c+3 of the workgroup's (gate) rows.  A lane's accumulator

@@ -107,20 +107,29 @@ def main():
                     continue
                 x = (torch.rand(m, k, device=dev, generator=g) * 2 - 1).to(torch.bfloat16)
                 resid = (torch.rand(m, n, device=dev, generator=g) * 2 - 1).to(torch.bfloat16) if mode == 2 else None
+                # TP=1 consumers (QKV, gate_up, LM head) read the residual stream with the norm folded in: the hand-
+                # written kernels scale rows by the producer's partials (NORMP), the library path runs the RMSNorm
+                # kernel first — time both as the model runs them
+                normp = model == "8b" and mode in (0, 1)
+                part = (x.float() ** 2).view(m, 64, -1).sum(-1).contiguous() if normp else None
+                ones = torch.ones(k, device=dev, dtype=torch.bfloat16)
 
                 def lib(i):
-                    y = x @ ws[i % ncopy].t()
+                    xin = ops.rmsnorm(x, ones, 1e-5) if normp else x
+                    y = xin @ ws[i % ncopy].t()
                     return ops.silu_mul(y) if mode == 1 else (y + resid if mode == 2 else y)
 
                 def own(i, c):
                     if c[0] == "gemv":
                         if mode == 2:
                             return G.gemv_resid(x, ws[i % ncopy], resid).s
+                        if normp:
+                            return torch.ops.chronos.gemv_normp(x, part, 1e-5, ws[i % ncopy], mode == 1)
                         return G._gemv(x, ws[i % ncopy], mode == 1)
                     if c[0] >= G.SK_BASE:
                         return torch.ops.chronos.gemm_skinny(x, ws[i % ncopy], mode, c[0] - G.SK_BASE, c[1], resid,
-                                                             None, 1e-5)[0]
-                    return torch.ops.chronos.gemm_pp(x, ws[i % ncopy], mode, c[0], c[1], resid, None, 1e-5, False)[0]
+                                                             part, 1e-5)[0]
+                    return torch.ops.chronos.gemm_pp(x, ws[i % ncopy], mode, c[0], c[1], resid, part, 1e-5, False)[0]
 
                 if m == 1:
                     if not G.gemv_ok(m, n, k):
