@@ -81,3 +81,22 @@ def test_mixed_steps_match_teacher_forcing_and_plain_scheduling():
         outs.append([r.out_ids for r in reqs])
         assert eng.blocks.free == eng.blocks.num_blocks - 1 and not eng.running
     assert outs[0] == outs[1]
+
+
+def test_wave_backlog_prefills_in_full_steps():
+    """A wave (more queued prompts than mixed_max_backlog) is prefilled in full-size steps; mixing resumes once the
+    backlog is a trickle."""
+    from chronos.sensor.prompt import VERDICT_SCHEMA
+
+    eng = _engine(max_slots=8, mixed_max_backlog=4, mixed_prefill_tokens=48, mixed_ratio=1)
+    prompts = _chains(12)
+    reqs = [eng.submit(p, fmt=VERDICT_SCHEMA, num_predict=20) for p in prompts]
+    seen = []
+    while eng.has_work():
+        backlog = len(eng.waiting) + len(eng.prefilling)
+        m0, p0 = eng.stats["mixed_steps"], eng.stats["prefill_steps"]
+        eng.step()
+        if eng.stats["mixed_steps"] > m0:
+            seen.append(backlog)
+    assert seen and max(seen) <= 4
+    assert all(r.done_reason in ("stop", "length") for r in reqs)
