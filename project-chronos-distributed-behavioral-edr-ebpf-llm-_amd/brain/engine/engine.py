@@ -101,11 +101,13 @@ class EngineConfig:
     mixed_batching: bool = True
     mixed_prefill_tokens: int = 2048
     mixed_ratio: int = 4
-    # ... but only for a trickle of arrivals: with more than this many prompts queued or prefilling (a wave of chains
-    # arriving together) full-size prefill steps clear the backlog first — 2048-token mixed chunks would re-stream
-    # every weight once per chunk (wave of 1024 chains: 17 forwards instead of 4, 575 vs 620 chains/s), while the
-    # steady state gains from mixing (closed loop at 1024 streams: 691 vs 590 chains/s; profiles/r3_bench_mixed_ab)
-    mixed_max_backlog: int = 64
+    # ... but only while the arrivals are a stream, not a wave: with more than this many prompts queued or
+    # prefilling (a wave of chains arriving together) full-size prefill steps clear the backlog first — 2048-token
+    # mixed chunks would re-stream every weight once per chunk (wave of 1024 chains: 17 forwards instead of 4, 575 vs
+    # 620 chains/s), while the steady state gains from mixing (closed loop at 1024 streams: 691 vs 590 chains/s;
+    # profiles/r3_bench_mixed_ab.txt).  A closed loop's harvests return ~100 completions (and as many arrivals) at
+    # once; a limit of 64 turned most of them back into plain prefill steps (619 chains/s).
+    mixed_max_backlog: int = 256
     # token automata compiled at start-up (a first request must not pay the ~4 s vocab walk: the reference's cold-start
     # timeout): "verdict" = the CHRONOS verdict schema the sensor sends, "json" = format:"json"
     warm_formats: tuple = ("verdict", "json")
