@@ -180,23 +180,46 @@ __global__ void __launch_bounds__(256) rope_kv_write_kernel(
 // ------------------------------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) silu_mul_kernel(const uint16_t* __restrict__ gu, uint16_t* __restrict__ out,
                                                        int64_t rows, int f) {
-    const int nv = f / 8;
-    const int64_t total = rows * nv;
-    for (int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < total;
-         idx += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t r = idx / nv;
-        const int c = (int)(idx - r * nv);
-        const u16x8 g = reinterpret_cast<const u16x8*>(gu + r * 2 * f)[c];
-        const u16x8 u = reinterpret_cast<const u16x8*>(gu + r * 2 * f + f)[c];
-        u16x8 o;
+    // one thread = 2 consecutive 8-element chunks of a row (f % 16 == 0), all four loads issued before any math: the
+    // M = 1024 decode shape (1024 x 14336) ran 26 us as a capped grid-stride loop with one chunk per iteration, i.e.
+    // ~3.4 TB/s on 88 MB
+    const int np = f / 16;  // chunk pairs per row
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= rows * np) return;
+    const int64_t r = idx / np;
+    const int c = 2 * (int)(idx - r * np);
+    const u16x8* g = reinterpret_cast<const u16x8*>(gu + r * 2 * f);
+    const u16x8* u = reinterpret_cast<const u16x8*>(gu + r * 2 * f + f);
+    const u16x8 g0 = g[c], g1 = g[c + 1], u0 = u[c], u1 = u[c + 1];
+    u16x8 o0, o1;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const float x = bf2f(g[j]);
-            const float sx = bf2f(f2bf(x / (1.f + __expf(-x))));
-            o[j] = f2bf(sx * bf2f(u[j]));
-        }
-        reinterpret_cast<u16x8*>(out + r * f)[c] = o;
+    for (int j = 0; j < 8; ++j) {
+        const float x0 = bf2f(g0[j]), x1 = bf2f(g1[j]);
+        o0[j] = f2bf(bf2f(f2bf(x0 / (1.f + __expf(-x0)))) * bf2f(u0[j]));
+        o1[j] = f2bf(bf2f(f2bf(x1 / (1.f + __expf(-x1)))) * bf2f(u1[j]));
     }
+    u16x8* ov = reinterpret_cast<u16x8*>(out + r * f);
+    ov[c] = o0;
+    ov[c + 1] = o1;
+}
+
+// f % 16 != 0: one chunk per thread
+__global__ void __launch_bounds__(256) silu_mul1_kernel(const uint16_t* __restrict__ gu, uint16_t* __restrict__ out,
+                                                        int64_t rows, int f) {
+    const int nv = f / 8;
+    const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= rows * nv) return;
+    const int64_t r = idx / nv;
+    const int c = (int)(idx - r * nv);
+    const u16x8 g = reinterpret_cast<const u16x8*>(gu + r * 2 * f)[c];
+    const u16x8 u = reinterpret_cast<const u16x8*>(gu + r * 2 * f + f)[c];
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float x = bf2f(g[j]);
+        o[j] = f2bf(bf2f(f2bf(x / (1.f + __expf(-x)))) * bf2f(u[j]));
+    }
+    reinterpret_cast<u16x8*>(out + r * f)[c] = o;
 }
 
 // ------------------------------------------------------------------------------------------------------------------
@@ -242,10 +265,13 @@ void launch_rope_kv_write(const uint16_t* qkv, const int32_t* pos, const int32_t
 
 void launch_silu_mul(const uint16_t* gu, uint16_t* out, int64_t rows, int f, hipStream_t st) {
     if (rows == 0) return;
-    const int64_t total = rows * (f / 8);
-    int64_t blocks = (total + 255) / 256;
-    if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(silu_mul_kernel, dim3((unsigned)blocks), dim3(256), 0, st, gu, out, rows, f);
+    const bool pairs = f % 16 == 0;
+    const int64_t total = rows * (pairs ? f / 16 : f / 8);
+    const int64_t blocks = (total + 255) / 256;
+    if (pairs)
+        hipLaunchKernelGGL(silu_mul_kernel, dim3((unsigned)blocks), dim3(256), 0, st, gu, out, rows, f);
+    else
+        hipLaunchKernelGGL(silu_mul1_kernel, dim3((unsigned)blocks), dim3(256), 0, st, gu, out, rows, f);
 }
 
 }  // namespace chronos
