@@ -228,7 +228,7 @@ def attn_o(q, k_cache, v_cache, block_table, ctx_len, w, resid, scale: float, gr
     if _checking(q):
         _check_paged(block_table[:1], k_cache, torch.arange(1), ctx_len[:1], "attn_o")
     s, part = _k().attn_o(q, k_cache, v_cache, block_table, ctx_len, w, resid, scale, grid_cap)
-    if s.numel() == 0:
+    if s is None or s.numel() == 0:  # declined (an undefined tensor comes back as None)
         return None
     return ResidOut(s, part)
 
