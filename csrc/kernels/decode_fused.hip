@@ -49,6 +49,8 @@ struct AttnOArgs {
     int* sync;              // [2]: attention arrivals, finished workgroups (zero between launches)
     int* err;               // set when a wait timed out
     int spin_limit;
+    int pre;                // weight ring entries (of DEPTH) issued before the wait (knob attn_o_pre)
+    int sleep;              // s_sleep(1) repetitions between polls (knob attn_o_sleep)
     const int32_t* gst;     // decode gate (see chronos_hip.h)
     int gn;
 };
@@ -248,16 +250,20 @@ __global__ void __launch_bounds__(256) attn_o_kernel(AttnOArgs a) {
         for (int d = 0; d < DEPTH; ++d)
             if (w + 4 * d < nchunk) load(w + 4 * d, d);
     };
+    // the first ring: a.pre entries before the wait (they stream while the attention runs; more of them compete with
+    // the attention's own K/V reads for HBM), the rest after it
     if (g < ntasks) {
         set_rows(g);
-        prologue();
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d)
+            if (d < a.pre && w + 4 * d < nchunk) load(w + 4 * d, d);
     }
     // wait for the attention output, then stage it in LDS (every workgroup, also those without a task: they still
     // count as finished below)
     if (threadIdx.x == 0) {
         int ok = 1, n = 0;
         while (__hip_atomic_load(a.sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.hkv) {
-            __builtin_amdgcn_s_sleep(1);
+            for (int z = 0; z < a.sleep; ++z) __builtin_amdgcn_s_sleep(1);
             if (++n > a.spin_limit) {
                 ok = 0;
                 break;
@@ -269,6 +275,11 @@ __global__ void __launch_bounds__(256) attn_o_kernel(AttnOArgs a) {
         s_ok = ok;
     }
     __syncthreads();
+    if (g < ntasks) {
+#pragma unroll
+        for (int d = 0; d < DEPTH; ++d)
+            if (d >= a.pre && w + 4 * d < nchunk) load(w + 4 * d, d);
+    }
     for (int i = threadIdx.x; i < K / 8; i += 256)
         reinterpret_cast<u16x8*>(xs)[i] = reinterpret_cast<const u16x8*>(a.attn_out)[i];
     __syncthreads();
@@ -339,6 +350,7 @@ bool launch_attn_o(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, co
                    int* err, int grid_cap, hipStream_t st) {
     constexpr int R = 4, DEPTH = 3, KMAX = 8192;
     if (K != hq * kHd || K % 512 || K > KMAX || N % R || hq % hkv || hkv > 64) return false;
+    if (!knob("attn_o", 1)) return false;  // in-process A/B: 0 = the separate kernels
     AttnOArgs a{};
     a.q = q;
     a.kc = kc;
@@ -359,12 +371,15 @@ bool launch_attn_o(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, co
     a.sync = sync;
     a.err = err;
     a.spin_limit = knob("attn_o_spin", 1 << 22);
+    a.pre = knob("attn_o_pre", DEPTH);
+    a.sleep = knob("attn_o_sleep", 1);
     const int32_t* gst = g_gate_n > 0 && g_gate_n <= kGateMax ? g_gate_state : nullptr;
     a.gst = gst;
     a.gn = gst ? -g_gate_n : 0;
     const int ntasks = N / R;
     const int fit = resident_workgroups(attn_o_kernel<R, DEPTH, KMAX>, 256);
     int grid = fit < ntasks ? fit : ntasks;
+    if (grid_cap <= 0) grid_cap = knob("attn_o_grid", 0);
     if (grid_cap > 0 && grid_cap < grid) grid = grid_cap;
     if (grid < hkv) grid = hkv;
     hipLaunchKernelGGL((attn_o_kernel<R, DEPTH, KMAX>), dim3(grid), dim3(256), 0, st, a);
