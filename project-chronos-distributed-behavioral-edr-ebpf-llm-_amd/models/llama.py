@@ -31,8 +31,9 @@ _FUSE_NORM = os.environ.get("CHRONOS_FUSE_NORM", "1") != "0"
 _FUSE_AR_NORM = os.environ.get("CHRONOS_FUSE_AR_NORM", "1") != "0"  # TP: fused IPC all-reduce + residual + RMSNorm
 # batched decode (>= 2048 (row, kv head) items, bf16 KV): RoPE + paged-KV write fused into the decode attention
 _FUSE_DECODE_ROPE = os.environ.get("CHRONOS_FUSE_DECODE_ROPE", "1") != "0"
-# single stream (T = 1, TP = 1, bf16 KV): attention + O GEMV + residual epilogue in one persistent launch
-_FUSE_ATTN_O = os.environ.get("CHRONOS_FUSE_ATTN_O", "1") != "0"
+# single stream (T = 1, TP = 1, bf16 KV): attention + O GEMV + residual epilogue in one persistent launch.  Off by
+# default: first measurement 3.04 ms/token against 2.81 for the separate kernels (profiles/r3_attn_o_ab.*)
+_FUSE_ATTN_O = os.environ.get("CHRONOS_FUSE_ATTN_O", "0") == "1"
 
 
 @dataclass

@@ -98,7 +98,7 @@ def test_single_stream_engine_same_tokens_fused_or_not(monkeypatch):
 
     outs = {}
     for fused in (False, True):
-        monkeypatch.setattr(llama, "_FUSE_ATTN_O", fused)
+        monkeypatch.setattr(llama, "_FUSE_ATTN_O", fused)  # explicit: the model default is off
         eng = Engine(EngineConfig(model="small", device="cuda", max_slots=2, max_model_len=384, decode_burst=4,
                                   seed=0, jump_forward=False))
         req = eng.submit(build_prompt(["[OPEN] attack_chain.sh -> /tmp/malware.bin",
