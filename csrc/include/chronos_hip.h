@@ -27,6 +27,26 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
     return __builtin_bit_cast(uint16_t, b);
 }
 
+// Write-through (sc1) stores and L1-bypassing sc1 loads of a 16-byte fp32 vector, for hand-offs between workgroups
+// that need no release / acquire fence (MI355X_MICROARCH.md hand-off table, first row: every store of the handed-off
+// bytes sc1, one lane per storing workgroup signals with an agent-scope atomic after all its waves' vmcnt(0) and a
+// barrier, every load of them sc1 after the signal was seen).  Vector memory instructions only.
+__device__ __forceinline__ void st_wt(float* p, const f32x4& v) {
+    typedef float f32x2v __attribute__((ext_vector_type(2)));
+    uint64_t* q = reinterpret_cast<uint64_t*>(p);
+    __hip_atomic_store(q, __builtin_bit_cast(uint64_t, f32x2v{v[0], v[1]}), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(q + 1, __builtin_bit_cast(uint64_t, f32x2v{v[2], v[3]}), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ f32x4 ld_wt(const float* p) {
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(p);
+    f32x4 v;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        v[i] = __uint_as_float(__hip_atomic_load(q + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    return v;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

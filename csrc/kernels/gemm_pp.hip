@@ -22,7 +22,8 @@
 //     late as the barrier before the stage's first reader allows (group 0 after its MFMA block, group 1 after its
 //     reads), and only raw s_barrier is used (never __syncthreads, which would drain the ring);
 //   * split-K (decode shapes whose tile grid under-fills 256 CUs): each K slice writes an fp32 slab in register
-//     order, takes an agent-scope ticket (release fence before, acquire fence in the last arriver —
+//     order with write-through (sc1) stores, takes an agent-scope ticket (no fences: the slab loads of the last
+//     arriver are sc1 too, chronos_hip.h st_wt / ld_wt —
 //     cdna_hip_programming.md §5 "In-launch split-K reduction"), and the last arriver of a tile sums the slabs and
 //     runs the epilogue;
 //   * XCD-aware task order: a tile's split-K slices and the x-row tiles of one W panel are consecutive task ids,
@@ -336,20 +337,14 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(PPArgs a) {
         for (int s = 0; s < NT; ++s)
 #pragma unroll
             for (int t = 0; t < MT; ++t)
-                *reinterpret_cast<f32x4*>(slab + (((wave * NT + s) * MT + t) * 64 + lane) * 4) = acc[s][t];
+                st_wt(slab + (((wave * NT + s) * MT + t) * 64 + lane) * 4, acc[s][t]);  // write-through (no fences)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         int* flag = reinterpret_cast<int*>(smem + EXTRA);
         if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             const int old = __hip_atomic_fetch_add(a.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const int last = old == S - 1;
-            if (last) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __hip_atomic_store(a.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
+            if (last) __hip_atomic_store(a.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             *flag = last;
         }
         __syncthreads();
@@ -362,7 +357,7 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(PPArgs a) {
             for (int s = 0; s < NT; ++s)
 #pragma unroll
                 for (int t = 0; t < MT; ++t) {
-                    const f32x4 v = *reinterpret_cast<const f32x4*>(sl + (((wave * NT + s) * MT + t) * 64 + lane) * 4);
+                    const f32x4 v = ld_wt(sl + (((wave * NT + s) * MT + t) * 64 + lane) * 4);
                     acc[s][t] = o == 0 ? v : acc[s][t] + v;
                 }
         }

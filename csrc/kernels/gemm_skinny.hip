@@ -19,8 +19,9 @@
 //     counted waits retire the oldest unit only);
 //   * MT x tiles of 16 rows (M <= 16 MT), RT W tiles: x bytes / W bytes = MT / RT per wave, kept <= 2 so the TCP
 //     carries the weight stream plus the x re-reads;
-//   * the NW waves' accumulators meet in LDS (fixed order), optional split-K across workgroups through fp32 slabs with
-//     an agent-scope ticket whose last arriver sums the slabs in slice order (bitwise reproducible, graph == eager);
+//   * the NW waves' accumulators meet in LDS (fixed order), optional split-K across workgroups through write-through
+//     fp32 slabs and an agent-scope ticket whose last arriver sums the slabs in slice order (no fences; bitwise
+//     reproducible, graph == eager);
 //   * epilogue per (row m, 4 consecutive outputs): 8-byte stores, CPR consecutive lanes cover a row's 16 RT outputs.
 #include "chronos_gemm.h"
 #include "chronos_hip.h"
@@ -169,38 +170,35 @@ __global__ void __launch_bounds__(64 * NW) skinny_kernel(PPArgs a) {
     }
 
     if (S > 1) {  // split-K: slab per task in output-unit order, ticket per row group, last arriver sums in order
+        // fence-free hand-off (chronos_hip.h st_wt / ld_wt): write-through slab stores, one lane's ticket after every
+        // wave drained its stores, sc1 slab loads by the last arriver — an agent release + acquire pair per workgroup
+        // (an L2 write-back + an L1 invalidate) cost 15-25 us on the decode shapes, more than the split saved
         constexpr int SLAB = NOUT * PAIR;  // f32x4 per task
-        f32x4* slab = reinterpret_cast<f32x4*>(a.ws) + (int64_t)task * SLAB;
+        float* slab = a.ws + (int64_t)task * SLAB * 4;
         if (active) {
 #pragma unroll
             for (int j = 0; j < VP; ++j)
 #pragma unroll
-                for (int p = 0; p < PAIR; ++p) slab[(tid + NT * j) * PAIR + p] = val[j][p];
+                for (int p = 0; p < PAIR; ++p) st_wt(slab + ((tid + NT * j) * PAIR + p) * 4, val[j][p]);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             const int old = __hip_atomic_fetch_add(a.cnt + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const int last = old == S - 1;
-            if (last) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __hip_atomic_store(a.cnt + g, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
+            if (last) __hip_atomic_store(a.cnt + g, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             *flag = last;
         }
         __syncthreads();
         if (!*flag) return;
         if (active) {
-            const f32x4* base = reinterpret_cast<const f32x4*>(a.ws) + (int64_t)g * S * SLAB;
+            const float* base = a.ws + (int64_t)g * S * SLAB * 4;
             for (int o = 0; o < S; ++o) {
 #pragma unroll
                 for (int j = 0; j < VP; ++j)
 #pragma unroll
                     for (int p = 0; p < PAIR; ++p) {
-                        const f32x4 v = base[(int64_t)o * SLAB + (tid + NT * j) * PAIR + p];
+                        const f32x4 v = ld_wt(base + ((int64_t)o * SLAB + (tid + NT * j) * PAIR + p) * 4);
                         val[j][p] = o == 0 ? v : val[j][p] + v;
                     }
             }
