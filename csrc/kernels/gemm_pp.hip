@@ -22,8 +22,8 @@
 //     late as the barrier before the stage's first reader allows (group 0 after its MFMA block, group 1 after its
 //     reads), and only raw s_barrier is used (never __syncthreads, which would drain the ring);
 //   * split-K (decode shapes whose tile grid under-fills 256 CUs): each K slice writes an fp32 slab in register
-//     order with write-through (sc1) stores, takes an agent-scope ticket (no fences: the slab loads of the last
-//     arriver are sc1 too, chronos_hip.h st_wt / ld_wt —
+//     order — write-through (sc1) stores and no fences for slabs up to 64 KiB (chronos_hip.h st_wt / ld_wt), plain
+//     stores + an agent release / acquire pair for bigger ones — takes an agent-scope ticket (
 //     cdna_hip_programming.md §5 "In-launch split-K reduction"), and the last arriver of a tile sums the slabs and
 //     runs the epilogue;
 //   * XCD-aware task order: a tile's split-K slices and the x-row tiles of one W panel are consecutive task ids,
@@ -330,21 +330,38 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(PPArgs a) {
     }
     if (g == 0) pp_bar();
 
-    // ---- split-K: slab, ticket, last arriver sums
+    // ---- split-K: slab, ticket, last arriver sums.  Slabs up to 64 KiB per task (128 x 128 tiles) go write-through
+    // with no fences (2-5 us per split); bigger ones through plain stores + one release / acquire pair, which
+    // measured cheaper for 256 KiB slabs (down at M = 1024: 132 against 189 us; profiles/r3_gemm_table_*)
+    constexpr bool WT = BM * BN <= 128 * 128;
     if (S > 1) {
         float* slab = a.ws + (int64_t)task * (BM * BN);
 #pragma unroll
         for (int s = 0; s < NT; ++s)
 #pragma unroll
             for (int t = 0; t < MT; ++t)
-                st_wt(slab + (((wave * NT + s) * MT + t) * 64 + lane) * 4, acc[s][t]);  // write-through (no fences)
+            {
+                float* p = slab + (((wave * NT + s) * MT + t) * 64 + lane) * 4;
+                if constexpr (WT) st_wt(p, acc[s][t]);  // write-through: no fences
+                else *reinterpret_cast<f32x4*>(p) = acc[s][t];
+            }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         int* flag = reinterpret_cast<int*>(smem + EXTRA);
         if (tid == 0) {
+            if constexpr (!WT) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
             const int old = __hip_atomic_fetch_add(a.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const int last = old == S - 1;
-            if (last) __hip_atomic_store(a.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (last) {
+                if constexpr (!WT) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                __hip_atomic_store(a.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
             *flag = last;
         }
         __syncthreads();
@@ -357,7 +374,8 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(PPArgs a) {
             for (int s = 0; s < NT; ++s)
 #pragma unroll
                 for (int t = 0; t < MT; ++t) {
-                    const f32x4 v = ld_wt(sl + (((wave * NT + s) * MT + t) * 64 + lane) * 4);
+                    const float* p = sl + (((wave * NT + s) * MT + t) * 64 + lane) * 4;
+                    const f32x4 v = WT ? ld_wt(p) : *reinterpret_cast<const f32x4*>(p);
                     acc[s][t] = o == 0 ? v : acc[s][t] + v;
                 }
         }

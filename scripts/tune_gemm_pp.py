@@ -67,6 +67,13 @@ def candidates(m, n, k, mode, keep=6):
     for must in ((0, 1), (4, 1), (8, 1)):
         if must not in out and G._pp_valid(must[0], n, k, mode, 1):
             out.append(must)
+    # split-K of the widest tiles where the tile grid under-fills the chip (the fence-free split costs ~2-5 us)
+    for cfg in (0, 4, 3):
+        bm, bn = G._PP_BM[cfg], G._PP_BN[cfg]
+        tiles = -(-m // bm) * -(-n // bn)
+        for sk in (2, 3, 4, 8):
+            if tiles < 256 and tiles * sk <= 768 and G._pp_valid(cfg, n, k, mode, sk) and (cfg, sk) not in out:
+                out.append((cfg, sk))
     return out
 
 
