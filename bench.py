@@ -60,6 +60,8 @@ def parse():
     ap.add_argument("--async-harvest", action="store_true")
     ap.add_argument("--prefill-ramp", type=int, default=2048, help="first prefill step after idle (0 = full chunks)")
     ap.add_argument("--no-jump-forward", action="store_true", help="decode grammar-forced runs token by token")
+    ap.add_argument("--jump-max-rows", type=int, default=None,
+                    help="largest decode batch that parks rows for jump-forward (EngineConfig default if unset)")
     ap.add_argument("--no-mixed", action="store_true",
                     help="separate prefill steps (no prefill chunks riding in the decode batch's forward)")
     ap.add_argument("--mode", choices=["wave", "closed"], default="wave")
@@ -192,6 +194,7 @@ def main():
                        async_harvest=a.async_harvest, seed=0,
                        prefill_ramp=a.prefill_ramp, jump_forward=not a.no_jump_forward,
                        mixed_batching=not a.no_mixed,
+                       **({"jump_max_rows": a.jump_max_rows} if a.jump_max_rows is not None else {}),
                        weight_dtype=a.weights, tp_sequence_parallel=a.sequence_parallel)
     # TP: the ranks of a replica submit the same chains in the same order and step the same deterministic scheduler,
     # so they stay in lockstep by construction (the serving path adds the leader broadcast of parallel/tp_engine.py)
