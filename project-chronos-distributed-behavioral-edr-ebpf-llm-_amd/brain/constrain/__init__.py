@@ -59,6 +59,7 @@ class GrammarBank:
         self.used = 1
         self._host_dist: list[int] = [0]
         self._by_key: dict[str, CompiledGrammar] = {}
+        self._last = None  # (format object, its grammar): identity hit for a repeated schema object (never mutated)
         self._lock = threading.Lock()
         sample = b"\x00".join(token_bytes[:: max(1, len(token_bytes) // 4096)])
         self._fp = (vocab, len(token_bytes), self.stop_ids, max_string, json_depth, max_ws, hash(sample))
@@ -94,6 +95,16 @@ class GrammarBank:
         return cg.start
 
     def get(self, fmt) -> CompiledGrammar:
+        # a wave submits the same schema object for every chain: skip its canonical-JSON key (half of submit's cost)
+        last = self._last
+        if last is not None and last[0] is fmt:
+            return last[1]
+        cg = self._get(fmt)
+        if isinstance(fmt, dict):
+            self._last = (fmt, cg)  # the reference keeps the id from being reused by another object
+        return cg
+
+    def _get(self, fmt) -> CompiledGrammar:
         key = G.format_key(fmt if fmt not in ("", False) else None)
         with self._lock:
             if key in self._by_key:

@@ -110,6 +110,8 @@ def _fail_worker(rank, world, port, q):
             q.put((1, "returned"))
         except Exception as e:  # noqa: BLE001 — expected: the leader's process left the group
             q.put((1, "raised", type(e).__name__))
+        q.close()
+        q.join_thread()  # os._exit skips the queue's feeder thread: flush first
         os._exit(0)
     fatal = []
     svc = LockstepService(tpe, "llama3", idle_s=0.005, on_fatal=lambda e: fatal.append(str(e)))
@@ -133,6 +135,8 @@ def _fail_worker(rank, world, port, q):
     r1, r2 = asyncio.run(go())
     q.put((0, r1.done_reason, r2.done_reason, svc.broken, bool(fatal), calls[0]))
     svc.close()
+    q.close()
+    q.join_thread()
     os._exit(3)  # what the server's on_fatal hook does: the group restarts in fresh processes
 
 
