@@ -16,6 +16,7 @@ struct PPArgs {
     int32_t* cnt;           // split-K tickets, one per tile (zero between calls: the last arriver resets its own)
     int M, N, K, F, nparts_in, splitk, kts;
     float eps;
+    int gm;      // tile order: M-tiles per group (0 = every M-tile of a W panel consecutive); knob pp_gm
     int ablate;  // timing-only diagnostics (knob pp_ablate): 1 skip loop DMA, 2 skip LDS reads, 4 skip MFMA, 8 nt weights, 16/32 alias every W/x tile onto tile 0
 };
 

@@ -563,6 +563,7 @@ std::tuple<Tensor, Tensor> gemm_pp(const Tensor& x, const Tensor& w, int64_t mod
     a.kts = (int)(K / 64 / splitk);
     a.eps = (float)eps;
     a.ablate = chronos::knob("pp_ablate", 0);
+    a.gm = chronos::knob("pp_gm", 0);
     Tensor y = at::empty({M, mode == 1 ? N / 2 : N}, x.options());
     a.y = bfm(y);
     Tensor part_out;

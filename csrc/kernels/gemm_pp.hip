@@ -92,7 +92,19 @@ __global__ void __launch_bounds__(512, 2) gemm_pp_kernel(PPArgs a) {
     const int S = a.splitk;
     const int task = xcd_remap(blockIdx.x, mt * ntl * S);
     const int ks = task % S, tile = task / S;
-    const int tm = tile % mt, tn = tile / mt;
+    // tile order: with gm > 0 the M-tiles come in groups of gm, every W panel of a group before the next group, so
+    // the 32 tiles an XCD runs at once form a gm x (32 / gm) block that shares x rows AND W rows in its L2 (at large
+    // M the default order puts 32 different x tiles and one W panel there: every x byte then comes from beyond L2)
+    int tm, tn;
+    if (a.gm > 0 && mt > a.gm) {
+        const int per = a.gm * ntl, grp = tile / per, r = tile - grp * per;
+        const int gsz = min(a.gm, mt - grp * a.gm);
+        tm = grp * a.gm + r % gsz;
+        tn = r / gsz;
+    } else {
+        tm = tile % mt;
+        tn = tile / mt;
+    }
     const int m0 = tm * BM;
     const int NS = HALF ? 2 * a.kts : a.kts;  // stages of this task's K range
     const int64_t kbeg = (int64_t)ks * a.kts * 64;

@@ -52,8 +52,10 @@ def main():
     ap.add_argument("--warm", action="store_true")
     ap.add_argument("--prio", action="store_true")
     ap.add_argument("--only", default="", help="cfg:sk list, e.g. 0:1,1:2")
+    ap.add_argument("--gms", default="0", help="tile-order group sizes to sweep (knob pp_gm), e.g. 0,8")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
+    gms = [int(v) for v in args.gms.split(",")]
     from chronos import ops
 
     ops.load()
@@ -74,6 +76,7 @@ def main():
             if args.only:
                 keep = {tuple(int(v) for v in c.split(":")) for c in args.only.split(",")}
                 cands = [c for c in cands if c in keep]
+            cands = [(cfg, sk, gm) for cfg, sk in cands for gm in gms]
 
             def run_lib(i):
                 y = x @ ws[i % ncopy].t()
@@ -83,16 +86,17 @@ def main():
                     y = y + resid
                 return y
 
-            def run_pp(i, cfg, sk):
+            def run_pp(i, cfg, sk, gm):
+                torch.ops.chronos.set_knob("pp_gm", gm)
                 return torch.ops.chronos.gemm_pp(x, ws[i % ncopy], mode, cfg, sk, resid, None, 1e-5, args.prio)[0]
 
             # correctness first (vs the library, bf16 tolerance)
             ref = run_lib(0).float()
             scale = ref.abs().max().item()
             errs = {}
-            for cfg, sk in cands:
-                y = run_pp(0, cfg, sk).float()
-                errs[(cfg, sk)] = (y - ref).abs().max().item() / scale
+            for cfg, sk, gm in cands:
+                y = run_pp(0, cfg, sk, gm).float()
+                errs[(cfg, sk, gm)] = (y - ref).abs().max().item() / scale
             times = {("lib", 0): []}
             for c in cands:
                 times[c] = []
@@ -112,7 +116,7 @@ def main():
             lib_us = min(times[("lib", 0)])
             for key, ts in times.items():
                 us = min(ts)
-                row = dict(op=name, m=m, n=n, k=k, cand="hipblaslt" if key[0] == "lib" else f"cfg{key[0]}_sk{key[1]}",
+                row = dict(op=name, m=m, n=n, k=k, cand="hipblaslt" if key[0] == "lib" else f"cfg{key[0]}_sk{key[1]}" + (f"_gm{key[2]}" if key[2] else ""),
                            us=round(us, 2), us_med=round(sorted(ts)[len(ts) // 2], 2),
                            TF=round(flop / us / 1e6, 1), vs_lib=round(lib_us / us, 3),
                            rel_err=None if key[0] == "lib" else round(errs[key], 5), cold=not args.warm)

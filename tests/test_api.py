@@ -231,7 +231,7 @@ def test_dp_router_failover_and_respawn():
             ok_h, health = router.health()  # the fresh worker is still importing / building its engine
             done = []
             for t in tasks:
-                done.append(await asyncio.wait_for(t, 60))
+                done.append(await asyncio.wait_for(t, 240))  # the survivor runs 400-token requests on CPU
             failed = [i for i, d in enumerate(done) if d.done_reason == "error"]
             t_err = max(finished_at[i] for i in failed) - t_kill if failed else 99.0
             failed = [done[i] for i in failed]
