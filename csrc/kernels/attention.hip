@@ -378,7 +378,9 @@ __global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
     const int32_t* bt = block_table + (int64_t)seq * bt_stride;
     const int nblk = (ctx + block_size - 1) / block_size;
     int win = 0;
-    int btv = lane < nblk ? bt[lane] : 0;
+    // the first 64 block-table entries without waiting for ctx (entries past the context are never shuffled out):
+    // the table load, ctx and pos all issue together instead of as a ctx -> table dependent pair
+    int btv = lane < bt_stride ? bt[lane] : 0;
 
     const int nh = hq + 2 * hkv;  // RP: heads per token row of the QKV projection
     const int pnew = RP ? pos[seq] : 0;
@@ -417,7 +419,7 @@ __global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
         // that later loads it (K: lane (r = slot, h4); V^T: lane (r, h4 = slot / 4)), so same-thread ordering makes
         // the loop read the fresh values; no other wave touches this sequence's private last block.
         const int tn = pnew & (block_size - 1);
-        const int64_t blkn = bt[pnew / block_size];
+        const int64_t blkn = pnew / block_size < 64 ? __shfl(btv, pnew / block_size, 64) : bt[pnew / block_size];
         const uint16_t* row = q + (int64_t)seq * nh * kD;
         if (r == tn) {
             const uint16_t* kr = row + (int64_t)(hq + h) * kD + 8 * h4;

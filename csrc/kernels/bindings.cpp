@@ -563,7 +563,7 @@ std::tuple<Tensor, Tensor> gemm_pp(const Tensor& x, const Tensor& w, int64_t mod
     a.kts = (int)(K / 64 / splitk);
     a.eps = (float)eps;
     a.ablate = chronos::knob("pp_ablate", 0);
-    a.gm = chronos::knob("pp_gm", 0);
+    a.gm = chronos::knob("pp_gm", 8);  // +7-9 % at M = 16384 (profiles/r3_gemm_tile_order_m16384.jsonl)
     Tensor y = at::empty({M, mode == 1 ? N / 2 : N}, x.options());
     a.y = bfm(y);
     Tensor part_out;

@@ -84,6 +84,7 @@ class EngineConfig:
     tp_sequence_parallel: bool = False  # TP prefill: reduce-scatter / all-gather around the norms instead of all-reduce
     decode_gate: bool = True       # small buckets: kernels of steps after the last live row finished return at once
     cp_min_tokens: int = 4096      # context parallel (Engine(cp=...)): prefill chunks at least this long are split
+    cp_mode: str = "allgather"     # "allgather" (zigzag token pieces) or "ulysses" (head-sharded attention)
     # First prefill step after the engine was idle covers this many tokens, each later one 4x more, up to the chunk:
     # the GPU starts on a small chunk while the host tokenizes the next (0 = always full chunks).
     prefill_ramp: int = 2048
@@ -606,11 +607,12 @@ class Engine:
         ntok = sum(len(c) for c in chunks)
         if (self.cp.world > 1 and len(chunks) == 1
                 and ntok >= max(self.cfg.cp_min_tokens, 2 * self.cp.world)):  # context-parallel chunk
-            from ...parallel.context_parallel import last_logits, make_cp_batch
+            from ...parallel.context_parallel import last_logits, make_cp_batch, make_ulysses_batch
 
-            sb = make_cp_batch(chunks[0], starts[0], bts[0], self.model.cfg, self.cp, self.device,
-                               self.max_blocks_per_seq, nqt=self.cfg.prefill_nqt)
-            logits = last_logits(self.model.forward(sb, self.kv), self.cp)
+            build = make_ulysses_batch if self.cfg.cp_mode == "ulysses" else make_cp_batch
+            sb = build(chunks[0], starts[0], bts[0], self.model.cfg, self.cp, self.device,
+                       self.max_blocks_per_seq, nqt=self.cfg.prefill_nqt)
+            logits = last_logits(self.model.forward(sb, self.kv), self.cp, sb.cp)
             self.stats["cp_prefill_steps"] += 1
         else:
             chunks, starts, bts, reqs = self._fit(chunks, starts, bts, reqs)

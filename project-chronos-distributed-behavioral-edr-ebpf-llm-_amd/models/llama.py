@@ -604,6 +604,10 @@ class LlamaModel:
             cp = sb.cp
             ops.rope_kv_write(gather_kv(qkv, self.hq, cp), cp.pos_all, cp.seq_all, cp.bt, self.cos_sin,
                               cp.dummy_q, kv.k[li], kv.v[li], 0, self.hkv, False, kv.k_scale[li], kv.v_scale[li])
+        if sb.cp is not None and sb.cp.ulysses is not None:  # head-sharded attention of the whole chunk
+            from ..parallel.context_parallel import ulysses_attention
+
+            return ulysses_attention(q_buf, kv.k[li], kv.v[li], sb.cp, self.scale, kv.k_scale[li], kv.v_scale[li])
         if attn is None:
             attn = ops.paged_attention(q_buf, kv.k[li], kv.v[li], sb.block_table, sb.q_start, sb.ctx_len, sb.tiles,
                                        sb.ntiles, sb.nqt, sb.nsplit, self.scale, kv.k_scale[li], kv.v_scale[li])

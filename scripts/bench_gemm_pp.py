@@ -52,7 +52,7 @@ def main():
     ap.add_argument("--warm", action="store_true")
     ap.add_argument("--prio", action="store_true")
     ap.add_argument("--only", default="", help="cfg:sk list, e.g. 0:1,1:2")
-    ap.add_argument("--gms", default="0", help="tile-order group sizes to sweep (knob pp_gm), e.g. 0,8")
+    ap.add_argument("--gms", default="8", help="tile-order group sizes to sweep (knob pp_gm), e.g. 0,8")
     ap.add_argument("--out", default="")
     args = ap.parse_args()
     gms = [int(v) for v in args.gms.split(",")]

@@ -131,3 +131,59 @@ def test_dp2_bench_contract_on_two_gpus():
     assert len(lines) == 1, out.stdout
     r = json.loads(lines[0])
     assert r["n_gpus"] == 2 and r["config"]["parallelism"] == "dp2" and r["verdicts_valid"] == "16/16"
+
+
+def _cp_worker(rank, world, port, q, mode):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(rank)
+    res = {"ok": True, "msg": ""}
+    try:
+        import torch.distributed as dist
+
+        from chronos.brain.engine.engine import Engine
+        from chronos.parallel.tp import TPContext
+        from chronos.sensor.prompt import VERDICT_SCHEMA, build_prompt
+
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+        eng = Engine(_cp_cfg(f"cuda:{rank}", mode), cp=TPContext.from_group())
+        req = eng.submit(build_prompt(LONG_CHAIN), fmt=VERDICT_SCHEMA, num_predict=24)
+        eng.run_until_idle()
+        res.update(out=list(req.out_ids), text=req.text, cp_steps=eng.stats["cp_prefill_steps"])
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # noqa: BLE001
+        import traceback
+
+        res = {"ok": False, "msg": repr(e) + "\n" + traceback.format_exc()[-3000:]}
+    q.put((rank, res))
+
+
+LONG_CHAIN = [f"[OPEN] bash -> /var/lib/app/file_{i}.dat" for i in range(40)] + ["[EXEC] bash -> curl"]
+
+
+def _cp_cfg(device, mode="allgather"):
+    from chronos.brain.engine.engine import EngineConfig
+
+    return EngineConfig(model="tiny", device=device, max_slots=2, max_model_len=1024, use_graphs=True, decode_burst=4,
+                        max_prefill_tokens=128, cp_min_tokens=64, prefix_cache=False, cp_mode=mode, seed=0)
+
+
+@pytest.mark.parametrize("mode", ["allgather", "ulysses"])
+def test_cp_prefill_distinct_gpus(mode):
+    """Context-parallel long prefill over RCCL on two GPUs (both forms, SURVEY.md §2.4 C6 / §2.5 Ulysses): every
+    rank decodes the verdict a single-GPU engine decodes, in lockstep."""
+    _need(2)
+    from chronos.brain.engine.engine import Engine
+    from chronos.sensor.prompt import VERDICT_SCHEMA, build_prompt
+
+    ref = Engine(_cp_cfg("cuda:0"))
+    r0 = ref.submit(build_prompt(LONG_CHAIN), fmt=VERDICT_SCHEMA, num_predict=24)
+    ref.run_until_idle()
+    want = list(r0.out_ids)
+    del ref
+    torch.cuda.empty_cache()
+    got = _spawn(_cp_worker, 2, mode, timeout=400)
+    assert all(got.get(r, {}).get("ok") for r in range(2)), got
+    assert got[0]["out"] == got[1]["out"] and got[0]["cp_steps"] >= 1
+    json.loads(got[0]["text"])
+    assert got[0]["out"][:8] == want[:8]
