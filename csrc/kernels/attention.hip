@@ -343,8 +343,8 @@ __global__ void __launch_bounds__(256) paged_attn_combine_kernel(
 // workgroup barrier and no partial output.  The sequence's block-table entries are fetched 64 at a time into one
 // VGPR (lane i = entry i of the window) and read with a shuffle, instead of a dependent global load per 16 tokens.
 // With ~100-200-token verdict contexts the split-over-waves kernel above spent most of its time in those fixed
-// costs (one 32-token step per wave, then merge); this form is bound by the K/V bytes.  Same MFMA mapping and the
-// same per-step arithmetic order as paged_attn_kernel<1>.
+// costs (one 32-token step per wave, then merge); this form is bound by the K/V bytes.  The same MFMAs as
+// paged_attn_kernel<1> with the keys of a step permuted inside the MFMA (see load()), so results agree to rounding.
 // ------------------------------------------------------------------------------------------------------------------
 constexpr float kRescaleThrD = 8.f;  // decode LEAN defer-max threshold (log2 units)
 
@@ -421,7 +421,8 @@ __global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
         const int tn = pnew & (block_size - 1);
         const int64_t blkn = pnew / block_size < 64 ? __shfl(btv, pnew / block_size, 64) : bt[pnew / block_size];
         const uint16_t* row = q + (int64_t)seq * nh * kD;
-        if (r == tn) {
+        const int u = pnew & 31;  // the token's slot in its 32-token step (token <-> lane map: load() below)
+        if (r == 4 * (u >> 3) + (u & 3)) {
             const uint16_t* kr = row + (int64_t)(hq + h) * kD + 8 * h4;
             bf16x8 kn[4];
 #pragma unroll
@@ -431,7 +432,7 @@ __global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
 #pragma unroll
             for (int c = 0; c < 4; ++c) *reinterpret_cast<bf16x8*>(kdst + 32 * c) = kn[c];
         }
-        if (h4 == (tn >> 2)) {
+        if (h4 == (u >> 3)) {
             const uint16_t* vr = row + (int64_t)(hq + hkv + h) * kD + r;
             uint16_t* vdst = const_cast<uint16_t*>(vc) + ((blkn * hkv + h) * kD) * (int64_t)block_size + tn;
 #pragma unroll
@@ -439,43 +440,57 @@ __global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
         }
     }
 
-    auto load = [&](int t0, bf16x8 (&kf)[2][4], bf16x4 (&vf)[2][8]) {
+    // One 32-token step = pages A (tokens 0-15) and B (16-31).  Token <-> lane map, chosen so that every lane's 8 P
+    // values are 8 CONSECUTIVE tokens: MFMA g's row R holds token 8 (R >> 2) + 4 g + (R & 3), so lane (r, h4)'s
+    // accumulator i of S^T[g] is token 8 h4 + 4 g + i and its PV operand element j is token 8 h4 + j — one 16-B V^T
+    // load per (lane, 16 dims) instead of two 8-B ones (8 V loads per step instead of 16; the texture addresser was
+    // 70-75 % busy on the wave's decode shape, profiles/r3s2_decode_attn_pmc.txt).
+    auto load = [&](int t0, bf16x8 (&kf)[2][4], bf16x8 (&vf)[8]) {
+        if (t0 < ctx) {
+            const int bi = t0 / block_size;  // page A; t0 % 32 == 0, so A and B sit in one 64-entry window
+            while (bi >= win + 64) {  // wave-uniform: next window of 64 block-table entries
+                win += 64;
+                btv = win + lane < nblk ? bt[win + lane] : 0;
+            }
+            const int64_t blkA = __shfl(btv, bi - win, 64);
+            // past the context the B lanes re-read page A (valid memory); those tokens are masked in step()
+            const int64_t blkB = t0 + block_size < ctx ? (int64_t)__shfl(btv, bi + 1 - win, 64) : blkA;
+            const int64_t kblk = r < 8 ? blkA : blkB;
 #pragma unroll
-        for (int g = 0; g < 2; ++g) {
-            const int tg = t0 + 16 * g;
-            if (tg < ctx) {
-                const int bi = tg / block_size;
-                while (bi >= win + 64) {  // wave-uniform: next window of 64 block-table entries
-                    win += 64;
-                    btv = win + lane < nblk ? bt[win + lane] : 0;
-                }
-                const int64_t blk = __shfl(btv, bi - win, 64);
-                const int off = tg - bi * block_size;
-                const int64_t koff = (((blk * hkv + h) * block_size) + off + r) * kD + 8 * h4;
-                const int64_t voff = ((blk * hkv + h) * kD) * (int64_t)block_size + off + 4 * h4;
+            for (int g = 0; g < 2; ++g) {
+                const int off = (8 * (r >> 2) + 4 * g + (r & 3)) & (block_size - 1);
+                const int64_t koff = (((kblk * hkv + h) * block_size) + off) * kD + 8 * h4;
                 if constexpr (FP8) {
 #pragma unroll
                     for (int c = 0; c < 4; ++c) {
                         const uint2 v = *reinterpret_cast<const uint2*>(kc8 + koff + 32 * c);
                         kf[g][c] = fp8x8_to_bf16x8(v.x, v.y, k_scale);
                     }
-#pragma unroll
-                    for (int dt = 0; dt < 8; ++dt)
-                        vf[g][dt] = fp8x4_to_bf16x4(
-                            *reinterpret_cast<const uint32_t*>(vc8 + voff + (int64_t)(dt * 16 + r) * block_size), v_scale);
                 } else {
 #pragma unroll
                     for (int c = 0; c < 4; ++c) kf[g][c] = *reinterpret_cast<const bf16x8*>(kc + koff + 32 * c);
+                }
+            }
+            const int64_t vblk = h4 < 2 ? blkA : blkB;
+            const int64_t voff = ((vblk * hkv + h) * kD) * (int64_t)block_size + 8 * (h4 & 1);
+            if constexpr (FP8) {
 #pragma unroll
-                    for (int dt = 0; dt < 8; ++dt)
-                        vf[g][dt] = *reinterpret_cast<const bf16x4*>(vc + voff + (int64_t)(dt * 16 + r) * block_size);
+                for (int dt = 0; dt < 8; ++dt) {
+                    const uint2 v = *reinterpret_cast<const uint2*>(vc8 + voff + (int64_t)(dt * 16 + r) * block_size);
+                    vf[dt] = fp8x8_to_bf16x8(v.x, v.y, v_scale);
                 }
             } else {
 #pragma unroll
+                for (int dt = 0; dt < 8; ++dt)
+                    vf[dt] = *reinterpret_cast<const bf16x8*>(vc + voff + (int64_t)(dt * 16 + r) * block_size);
+            }
+        } else {
+#pragma unroll
+            for (int g = 0; g < 2; ++g)
+#pragma unroll
                 for (int c = 0; c < 4; ++c) kf[g][c] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
-                for (int dt = 0; dt < 8; ++dt) vf[g][dt] = bf16x4{0, 0, 0, 0};
-            }
+            for (int dt = 0; dt < 8; ++dt) vf[dt] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
         }
     };
 
@@ -484,15 +499,13 @@ __global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
 #pragma unroll
     for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    auto step = [&](int t0, bf16x8 (&kf)[2][4], bf16x4 (&vf)[2][8]) {
+    auto step = [&](int t0, bf16x8 (&kf)[2][4], bf16x8 (&vf)[8]) {
         if (t0 + 32 > ctx) {  // partial step: zero V of keys past the end (uniform branch)
 #pragma unroll
-            for (int g = 0; g < 2; ++g)
+            for (int j = 0; j < 8; ++j)
+                if (t0 + 8 * h4 + j >= ctx)
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    if (t0 + 16 * g + 4 * h4 + i >= ctx)
-#pragma unroll
-                        for (int dt = 0; dt < 8; ++dt) vf[g][dt][i] = (__bf16)0.f;
+                    for (int dt = 0; dt < 8; ++dt) vf[dt][j] = (__bf16)0.f;
         }
         f32x4 s[2];
 #pragma unroll
@@ -511,11 +524,11 @@ __global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
             // scale applied to the max and fused into the exponent's fma, raw v_exp_f32, and the defer-max rescale
             // (O and l rescaled only when the max grows past kRescaleThrD in log2 units: p <= 2^8 otherwise).
             if (t0 + 32 > ctx) {
-                const int lim = ctx - (t0 + 4 * h4);
+                const int lim = ctx - (t0 + 8 * h4);
 #pragma unroll
                 for (int g = 0; g < 2; ++g)
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) s[g][i] = (16 * g + i) >= lim ? -INFINITY : s[g][i];
+                    for (int i = 0; i < 4; ++i) s[g][i] = (4 * g + i) >= lim ? -INFINITY : s[g][i];
             }
 #pragma unroll
             for (int g = 0; g < 2; ++g)
@@ -541,10 +554,7 @@ __global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
                 }
             lsum = lsum * alpha + ps;
 #pragma unroll
-            for (int dt = 0; dt < 8; ++dt) {
-                const bf16x8 va = __builtin_shufflevector(vf[0][dt], vf[1][dt], 0, 1, 2, 3, 4, 5, 6, 7);
-                o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pf, o[dt], 0, 0, 0);
-            }
+            for (int dt = 0; dt < 8; ++dt) o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[dt], pf, o[dt], 0, 0, 0);
             return;
         }
 #pragma unroll
@@ -552,7 +562,7 @@ __global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 float v = s[g][i] * scale_log2;
-                if (t0 + 16 * g + 4 * h4 + i >= ctx) v = -INFINITY;
+                if (t0 + 8 * h4 + 4 * g + i >= ctx) v = -INFINITY;
                 s[g][i] = v;
                 mx = fmaxf(mx, v);
             }
@@ -573,14 +583,13 @@ __global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
 #pragma unroll
         for (int dt = 0; dt < 8; ++dt) {
             o[dt] *= alpha;
-            const bf16x8 va = __builtin_shufflevector(vf[0][dt], vf[1][dt], 0, 1, 2, 3, 4, 5, 6, 7);
-            o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pf, o[dt], 0, 0, 0);
+            o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[dt], pf, o[dt], 0, 0, 0);
         }
     };
 
     if constexpr (PF) {  // next step's K/V in flight while this one computes (two register sets, 1 wave/SIMD)
         bf16x8 kA[2][4], kB[2][4];
-        bf16x4 vA[2][8], vB[2][8];
+        bf16x8 vA[8], vB[8];
         load(0, kA, vA);
         for (int t0 = 0; t0 < ctx; t0 += 64) {
             if (t0 + 32 < ctx) load(t0 + 32, kB, vB);
@@ -591,7 +600,7 @@ __global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
         }
     } else {  // one register set: latency hidden by occupancy instead (3 waves/SIMD)
         bf16x8 kA[2][4];
-        bf16x4 vA[2][8];
+        bf16x8 vA[8];
         for (int t0 = 0; t0 < ctx; t0 += 32) {
             load(t0, kA, vA);
             step(t0, kA, vA);
