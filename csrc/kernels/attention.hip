@@ -355,7 +355,18 @@ constexpr float kRescaleThrD = 8.f;  // decode LEAN defer-max threshold (log2 un
 // raw [B, hq + 2 hkv, 128] QKV projection; the wave applies RoPE to its query rows in registers (every lane holds
 // both halves of its rotate-half pairs: dims 8 h4 + 32 c with c and c + 2) and writes the new token's (position
 // pos[seq], the last of the context) roped K and V into the cache before walking the context.
-template <bool FP8, bool PF, bool LEAN, int OCC, bool RP = false>
+typedef __attribute__((address_space(3))) void* pd_lds_ptr_t;
+typedef __attribute__((address_space(1))) void* pd_gbl_ptr_t;
+// dynamic LDS of the bf16 one-register-set variants: one 8 KiB K tile per wave + one 256-B row per wave parking the
+// fused-RoPE variant's new K row until its step
+constexpr int kPdKlds = 4 * 8192 + 4 * 256;
+
+// KLDS (bf16, one register set): a step's 32 K rows reach the wave through LDS-DMA (eight lane-linear 1 KiB pieces =
+// 4 whole 256-B rows each, into the wave's private 8 KiB, XOR-swizzled on the source address) and are read back in
+// the MFMA layout with conflict-free ds_read_b128.  Loaded straight into the MFMA layout each instruction touches 16
+// rows x 64 B, which the L2 -> CU path serves at ~18 B/clk per CU against ~60 for lane-linear LDS-DMA pieces
+// (csrc/microbench/l2_feed.hip, profiles/r3s2_decode_attn.md).
+template <bool FP8, bool PF, bool LEAN, int OCC, bool RP = false, bool KL = true>
 __global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
     const uint16_t* __restrict__ q, const void* __restrict__ kcv, const void* __restrict__ vcv,
     const int32_t* __restrict__ block_table, int bt_stride, const int32_t* __restrict__ ctx_len,
@@ -363,6 +374,8 @@ __global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
     const int32_t* __restrict__ gst, int gn, const int32_t* __restrict__ pos = nullptr,
     const float* __restrict__ cos_sin = nullptr) {
     static_assert(!(RP && FP8), "fused RoPE / KV write: bf16 KV only");
+    constexpr bool KLDS = KL && !FP8 && !PF;  // KL = false: K straight to VGPRs (A/B knob decode_klds)
+    extern __shared__ __attribute__((aligned(1024))) unsigned char pd_smem[];
     constexpr int block_size = 16;
     if (gate_closed(gst, gn)) return;  // the engine's page size; compile-time so every K/V address is base + immediate
     const int lane = threadIdx.x & 63;
@@ -374,6 +387,10 @@ __global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
     const uint8_t* vc8 = reinterpret_cast<const uint8_t*>(vcv);
     const int seq = item / hkv, h = item - seq * hkv;
     const int r = lane & 15, h4 = lane >> 4, G = hq / hkv;
+    unsigned char* kl = pd_smem + (threadIdx.x >> 6) * 8192;  // KLDS: this wave's K tile (32 rows x 256 B)
+    // KLDS swizzle: row t's 16-B chunk q sits in slot q ^ kswz(t); the fragment rows of one ds_read (8 (r >> 2) + 4 g
+    // + (r & 3), r = 0..15) map to kswz = r, 16 distinct slots of a 256-B bank row
+    auto kswz = [](int t) { return (t & 3) | ((t >> 3) << 2); };
     const int ctx = ctx_len[seq];
     const int32_t* bt = block_table + (int64_t)seq * bt_stride;
     const int nblk = (ctx + block_size - 1) / block_size;
@@ -414,6 +431,11 @@ __global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
         }
         if constexpr (RP) rope4(qf);
     }
+    // RP + KLDS: the new token's roped K is parked in the wave's spare LDS row (not in VGPRs) and copied into the K tile
+    // of its step after that step's DMA lands (the DMA may still fetch the pre-write bytes from the cache)
+    const int u = pnew & 31;  // the new token's slot in its 32-token step (token <-> lane map: load() below)
+    const bool kwriter = RP && r == 4 * (u >> 3) + (u & 3);
+    unsigned char* kpark = pd_smem + 4 * 8192 + (threadIdx.x >> 6) * 256;
     if constexpr (RP) {
         // The new token's K (roped) and V go to the cache before the loop.  Each element is written by the very lane
         // that later loads it (K: lane (r = slot, h4); V^T: lane (r, h4 = slot / 4)), so same-thread ordering makes
@@ -421,8 +443,7 @@ __global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
         const int tn = pnew & (block_size - 1);
         const int64_t blkn = pnew / block_size < 64 ? __shfl(btv, pnew / block_size, 64) : bt[pnew / block_size];
         const uint16_t* row = q + (int64_t)seq * nh * kD;
-        const int u = pnew & 31;  // the token's slot in its 32-token step (token <-> lane map: load() below)
-        if (r == 4 * (u >> 3) + (u & 3)) {
+        if (kwriter) {
             const uint16_t* kr = row + (int64_t)(hq + h) * kD + 8 * h4;
             bf16x8 kn[4];
 #pragma unroll
@@ -431,6 +452,10 @@ __global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
             uint16_t* kdst = const_cast<uint16_t*>(kc) + (((blkn * hkv + h) * block_size) + tn) * kD + 8 * h4;
 #pragma unroll
             for (int c = 0; c < 4; ++c) *reinterpret_cast<bf16x8*>(kdst + 32 * c) = kn[c];
+            if constexpr (KLDS) {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) *reinterpret_cast<bf16x8*>(kpark + (((4 * c + h4) ^ kswz(u)) << 4)) = kn[c];
+            }
         }
         if (h4 == (u >> 3)) {
             const uint16_t* vr = row + (int64_t)(hq + hkv + h) * kD + r;
@@ -455,9 +480,19 @@ __global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
             const int64_t blkA = __shfl(btv, bi - win, 64);
             // past the context the B lanes re-read page A (valid memory); those tokens are masked in step()
             const int64_t blkB = t0 + block_size < ctx ? (int64_t)__shfl(btv, bi + 1 - win, 64) : blkA;
+            if constexpr (KLDS) {
+                // piece i = step rows 4 i .. 4 i + 3, lane l -> row 4 i + (l >> 4), slot l & 15 <- chunk slot ^ kswz
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const int t = 4 * i + (lane >> 4);
+                    const int64_t pg = t < 16 ? blkA : blkB;
+                    const uint16_t* src = kc + (((pg * hkv + h) * block_size) + (t & 15)) * kD + 8 * ((lane & 15) ^ kswz(t));
+                    __builtin_amdgcn_global_load_lds((pd_gbl_ptr_t)src, (pd_lds_ptr_t)(kl + i * 1024), 16, 0, 0);
+                }
+            }
             const int64_t kblk = r < 8 ? blkA : blkB;
 #pragma unroll
-            for (int g = 0; g < 2; ++g) {
+            for (int g = 0; KLDS ? false : g < 2; ++g) {
                 const int off = (8 * (r >> 2) + 4 * g + (r & 3)) & (block_size - 1);
                 const int64_t koff = (((kblk * hkv + h) * block_size) + off) * kD + 8 * h4;
                 if constexpr (FP8) {
@@ -500,6 +535,22 @@ __global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
     for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     auto step = [&](int t0, bf16x8 (&kf)[2][4], bf16x8 (&vf)[8]) {
+        if constexpr (KLDS) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's K pieces are in LDS (and V in VGPRs)
+            if (RP && t0 == (pnew & ~31) && kwriter) {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const int o = ((4 * c + h4) ^ kswz(u)) << 4;
+                    *reinterpret_cast<bf16x8*>(kl + u * 256 + o) = *reinterpret_cast<const bf16x8*>(kpark + o);
+                }
+            }
+#pragma unroll
+            for (int g = 0; g < 2; ++g)
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    kf[g][c] = *reinterpret_cast<const bf16x8*>(kl + (8 * (r >> 2) + 4 * g + (r & 3)) * 256 +
+                                                                (((4 * c + h4) ^ r) << 4));
+        }
         if (t0 + 32 > ctx) {  // partial step: zero V of keys past the end (uniform branch)
 #pragma unroll
             for (int j = 0; j < 8; ++j)
@@ -633,12 +684,16 @@ bool launch_decode_attn_rope(const uint16_t* qkv, const int32_t* pos, const floa
         knob("decode_pf", 0) || !knob("decode_lean", 1) || !knob("decode_rope_fused", 1))
         return false;
     const float scale_log2 = scale * 1.4426950408889634f;
-    if (knob("decode_occ3", 1))
-        hipLaunchKernelGGL((paged_decode_kernel<false, false, true, 3, true>), dim3((nitems + 3) / 4), dim3(256), 0,
+    if (!knob("decode_klds", 1))
+        hipLaunchKernelGGL((paged_decode_kernel<false, false, true, 3, true, false>), dim3((nitems + 3) / 4),
+                           dim3(256), 0, st, qkv, kc, vc, block_table, bt_stride, ctx_len, out, nitems, hq, hkv,
+                           scale_log2, 1.f, 1.f, CHRONOS_GATE, pos, cos_sin);
+    else if (knob("decode_occ3", 1))
+        hipLaunchKernelGGL((paged_decode_kernel<false, false, true, 3, true>), dim3((nitems + 3) / 4), dim3(256), kPdKlds,
                            st, qkv, kc, vc, block_table, bt_stride, ctx_len, out, nitems, hq, hkv, scale_log2, 1.f,
                            1.f, CHRONOS_GATE, pos, cos_sin);
     else
-        hipLaunchKernelGGL((paged_decode_kernel<false, false, true, 1, true>), dim3((nitems + 3) / 4), dim3(256), 0,
+        hipLaunchKernelGGL((paged_decode_kernel<false, false, true, 1, true>), dim3((nitems + 3) / 4), dim3(256), kPdKlds,
                            st, qkv, kc, vc, block_table, bt_stride, ctx_len, out, nitems, hq, hkv, scale_log2, 1.f,
                            1.f, CHRONOS_GATE, pos, cos_sin);
     return true;
@@ -685,10 +740,15 @@ void launch_paged_attn(const uint16_t* q, const void* kc, const void* vc, const 
         const bool lean = knob("decode_lean", 1) != 0;
         const bool occ3 = knob("decode_occ3", 1) != 0;
 #define PD_LAUNCH(F, P, L, O)                                                                                   \
-    hipLaunchKernelGGL((paged_decode_kernel<F, P, L, O>), dim3((nitems + 3) / 4), dim3(256), 0, st, q, kc, vc,    \
+    hipLaunchKernelGGL((paged_decode_kernel<F, P, L, O>), dim3((nitems + 3) / 4), dim3(256), (!F && !P) ? kPdKlds : 0, \
+                       st, q, kc, vc,                                                                               \
                        block_table, bt_stride, ctx_len, out, nitems, hq, hkv, scale_log2, k_scale, v_scale, CHRONOS_GATE)
-#define PD_OCC(F, L)                     \
-    if (occ3) PD_LAUNCH(F, false, L, 3); \
+#define PD_OCC(F, L)                                                                                            \
+    if (!F && !knob("decode_klds", 1) && occ3)                                                                  \
+        hipLaunchKernelGGL((paged_decode_kernel<F, false, L, 3, false, false>), dim3((nitems + 3) / 4), dim3(256), \
+                           0, st, q, kc, vc, block_table, bt_stride, ctx_len, out, nitems, hq, hkv, scale_log2,   \
+                           k_scale, v_scale, CHRONOS_GATE);                                                       \
+    else if (occ3) PD_LAUNCH(F, false, L, 3);                                                                   \
     else PD_LAUNCH(F, false, L, 1);
         if (fp8) {
             if (pf) PD_LAUNCH(true, true, false, 1);
