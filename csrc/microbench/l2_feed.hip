@@ -57,6 +57,29 @@ __global__ void __launch_bounds__(512) feed(const unsigned char* __restrict__ sr
     if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) out[blockIdx.x] = 1;  // keeps the loads live
 }
 
+// HBM streaming (every byte read once, buffer >> the 256 MiB Infinity Cache): the same two VGPR layouts.  Each
+// workgroup walks 16-row x 8 KiB slabs of its own region; a pass = one 1 KiB instruction per wave per 1 KiB of slab.
+template <int MODE>
+__global__ void __launch_bounds__(512) stream(const unsigned char* __restrict__ src, unsigned* out, int slabs) {
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    u32x4 acc = {0, 0, 0, 0};
+    for (int sb = 0; sb < slabs; ++sb) {
+        const unsigned char* slab = src + ((size_t)blockIdx.x * slabs + sb) * 16 * kRowBytes;  // 128 KiB
+#pragma unroll 4
+        for (int i = 0; i < 16; ++i) {
+            const int piece = wave * 16 + i;  // 128 pieces of 1 KiB
+            const unsigned char* p;
+            if constexpr (MODE == 1) {  // 16 rows x 64 B (k slice piece)
+                p = slab + (size_t)(lane & 15) * kRowBytes + piece * 64 + 16 * (lane >> 4);
+            } else {  // 8 rows x 128 B
+                p = slab + (size_t)(8 * (piece & 1) + (lane >> 3)) * kRowBytes + (piece >> 1) * 128 + 16 * (lane & 7);
+            }
+            acc ^= *reinterpret_cast<const u32x4*>(p);
+        }
+    }
+    if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) out[blockIdx.x] = 1;
+}
+
 int main() {
     hipDeviceProp_t prop;
     hipGetDeviceProperties(&prop, 0);
@@ -86,6 +109,26 @@ int main() {
             const double tot = (double)cus * 65536.0 * iters;
             printf("%-34s %8.2f TB/s chip, %6.1f GB/s per CU (%.1f B/clk at 2.1 GHz)\n", names[mode],
                    tot / ms / 1e9, tot / cus / ms / 1e6, tot / cus / (ms * 1e-3) / 2.1e9);
+        }
+    }
+    // HBM: 256 workgroups x 24 slabs x 128 KiB = 768 MiB per launch
+    const int slabs = 24;
+    const size_t hb = (size_t)cus * slabs * 16 * kRowBytes;
+    unsigned char* big;
+    hipMalloc(&big, hb);
+    hipMemset(big, 1, hb);
+    const char* hn[2] = {"HBM VGPR fragment (16 rows x 64 B)", "HBM VGPR full lines (8 x 128 B)"};
+    for (int rep = 0; rep < 3; ++rep) {
+        for (int mode = 1; mode <= 2; ++mode) {
+            auto k = mode == 1 ? stream<1> : stream<2>;
+            hipLaunchKernelGGL(k, dim3(cus), dim3(512), 0, 0, big, out, slabs);
+            hipEventRecord(a);
+            hipLaunchKernelGGL(k, dim3(cus), dim3(512), 0, 0, big, out, slabs);
+            hipEventRecord(b);
+            hipEventSynchronize(b);
+            float ms;
+            hipEventElapsedTime(&ms, a, b);
+            printf("%-34s %8.2f TB/s chip\n", hn[mode - 1], hb / ms / 1e9);
         }
     }
     return 0;
