@@ -46,26 +46,34 @@ __global__ void __launch_bounds__(256) rmsnorm_kernel(const uint16_t* __restrict
     const u16x8* wv = reinterpret_cast<const u16x8*>(w);
     u16x8* yv = reinterpret_cast<u16x8*>(y + row * d);
     const int nv = d / 8;
+    // every load of the row (x, resid and the norm weight) issued before the first use: indices past the row are
+    // clamped (in-bounds re-reads) and masked, so hipcc does not branch around each load and wait per element
+    u16x8 a[MAXV], b[MAXV], g[MAXV];
+#pragma unroll
+    for (int k = 0; k < MAXV; ++k) {
+        const int i = min((int)threadIdx.x + k * 256, nv - 1);
+        a[k] = xv[i];
+        if constexpr (RESID) b[k] = rv[i];
+        g[k] = wv[i];
+    }
     float vals[MAXV][8];
     float ss = 0.f;
 #pragma unroll
     for (int k = 0; k < MAXV; ++k) {
         const int i = threadIdx.x + k * 256;
-        if (i < nv) {
-            u16x8 a = xv[i];
-            if constexpr (RESID) {
-                u16x8 b = rv[i];
-                u16x8 s;
+        if constexpr (RESID) {
+            u16x8 sv;
 #pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    s[j] = f2bf(bf2f(a[j]) + bf2f(b[j]));
-                    vals[k][j] = bf2f(s[j]);
-                }
-                rv[i] = s;
-            } else {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) vals[k][j] = bf2f(a[j]);
+            for (int j = 0; j < 8; ++j) {
+                sv[j] = f2bf(bf2f(a[k][j]) + bf2f(b[k][j]));
+                vals[k][j] = bf2f(sv[j]);
             }
+            if (i < nv) rv[i] = sv;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) vals[k][j] = bf2f(a[k][j]);
+        }
+        if (i < nv) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) ss += vals[k][j] * vals[k][j];
         }
@@ -76,9 +84,9 @@ __global__ void __launch_bounds__(256) rmsnorm_kernel(const uint16_t* __restrict
     for (int k = 0; k < MAXV; ++k) {
         const int i = threadIdx.x + k * 256;
         if (i < nv) {
-            u16x8 g = wv[i], o;
+            u16x8 o;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(f2bf(vals[k][j] * inv)) * bf2f(g[j]));
+            for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(f2bf(vals[k][j] * inv)) * bf2f(g[k][j]));
             yv[i] = o;
         }
     }
