@@ -23,6 +23,8 @@
 //     fp32 slabs and an agent-scope ticket whose last arriver sums the slabs in slice order (no fences; bitwise
 //     reproducible, graph == eager);
 //   * epilogue per (row m, 4 consecutive outputs): 8-byte stores, CPR consecutive lanes cover a row's 16 RT outputs.
+#include <algorithm>
+
 #include "chronos_gemm.h"
 #include "chronos_hip.h"
 
@@ -66,10 +68,28 @@ __global__ void __launch_bounds__(64 * NW) skinny_kernel(PPArgs a) {
             row = g * 16 * RT + 16 * rt;
         wp[rt] = reinterpret_cast<const bf16x8*>(a.w + (int64_t)(row + (lane & 15)) * K + kbase);
     }
+    // XL (MT >= 4, x bytes = MT / RT x the weight bytes): x is loaded in whole 128-B lines (lane l: row 8 i + l / 8,
+    // 16-B chunk l % 8 of the unit's 64 k) and turned into the MFMA B layout through the wave's private LDS tile
+    // (swizzled ds_write_b128, ds_read_b128).  Loads shaped like the MFMA operand (16 rows x 64 B per instruction)
+    // reach only ~18 B/clk per CU from L2 against ~50 for whole lines (csrc/microbench/l2_feed.hip): at M = 128 the x
+    // re-reads, not the weight stream, set the kernel time.
+    constexpr bool XL = MT >= 4;
     const bf16x8* xp[MT];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
-        xp[mt] = reinterpret_cast<const bf16x8*>(a.x + (int64_t)min(16 * mt + (lane & 15), M - 1) * K + kbase);
+    for (int mt = 0; mt < MT; ++mt) {
+        if constexpr (XL)  // pieces of 8 rows: xp[i] for i < 2 MT covers rows 8 i .. 8 i + 7
+            xp[mt] = nullptr;
+        else
+            xp[mt] = reinterpret_cast<const bf16x8*>(a.x + (int64_t)min(16 * mt + (lane & 15), M - 1) * K + kbase);
+    }
+    const bf16x8* xl[XL ? 2 * MT : 1];
+    if constexpr (XL) {
+#pragma unroll
+        for (int i = 0; i < 2 * MT; ++i)
+            xl[i] = reinterpret_cast<const bf16x8*>(a.x + (int64_t)min(8 * i + (lane >> 3), M - 1) * K + s * KS +
+                                                    wave * 64 + 8 * (lane & 7));
+    }
+    unsigned char* xs = smem + wave * (MT * 2048);  // XL: this wave's x tile, 16 MT rows x 128 B
 
     // unit u of this wave covers k = kbase + 64 NW u + {0, 32} (+ 8 (lane >> 4) already in the pointers)
     bf16x8 wr[D][RT][2], xr[D][MT][2];
@@ -82,8 +102,13 @@ __global__ void __launch_bounds__(64 * NW) skinny_kernel(PPArgs a) {
         }
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
-            xr[d][mt][0] = xp[mt][off];
-            xr[d][mt][1] = xp[mt][off + 4];
+            if constexpr (XL) {  // the same registers, in the line layout: piece 2 mt + h
+                xr[d][mt][0] = xl[2 * mt][off];
+                xr[d][mt][1] = xl[2 * mt + 1][off];
+            } else {
+                xr[d][mt][0] = xp[mt][off];
+                xr[d][mt][1] = xp[mt][off + 4];
+            }
         }
     };
 #pragma unroll
@@ -101,6 +126,26 @@ __global__ void __launch_bounds__(64 * NW) skinny_kernel(PPArgs a) {
         for (int d = 0; d < D; ++d) {
             const int u = u0 + d;
             if (u < NU) {
+                if constexpr (XL) {
+                    // line layout -> LDS (row t = 8 i + lane / 8, chunk lane % 8 in slot chunk ^ (t & 7)) -> MFMA layout
+                    // (row 16 mt + lane % 16, chunk 4 h + lane / 16); LDS ops of a wave run in order, so the previous
+                    // unit's reads are served before these writes
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            const int t = 8 * (2 * mt + h) + (lane >> 3);
+                            *reinterpret_cast<bf16x8*>(xs + t * 128 + (((lane & 7) ^ (t & 7)) << 4)) = xr[d][mt][h];
+                        }
+#pragma unroll
+                    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            const int t = 16 * mt + (lane & 15);
+                            xr[d][mt][h] = *reinterpret_cast<const bf16x8*>(
+                                xs + t * 128 + (((4 * h + (lane >> 4)) ^ (t & 7)) << 4));
+                        }
+                }
 #pragma unroll
                 for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -144,6 +189,7 @@ __global__ void __launch_bounds__(64 * NW) skinny_kernel(PPArgs a) {
     // Slots are padded by one per 16 (v + v/16): the lane-consecutive writes (unit stride CPR) and the
     // thread-consecutive reads (unit stride 1) both hit distinct banks.
     auto red_at = [&](int w, int p, int v) { return w * SZ + p * NP + v + (v >> 4); };
+    if constexpr (XL) __syncthreads();  // the slots alias the other waves' x tiles: every wave's main loop is done
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
@@ -256,7 +302,8 @@ __global__ void __launch_bounds__(64 * NW) skinny_kernel(PPArgs a) {
 template <int RT, int MT, int D, int NW, int MODE, bool NORMP>
 void launch_cfg(const PPArgs& a, hipStream_t st) {
     constexpr int UNITS = RT * MT * 64;
-    const int lds = NW * (UNITS + UNITS / 16) * 16 + 16 * MT * 4 + 16;
+    // the reduction slots (+ inv, flag) alias the XL x tiles, which are dead once the main loop ends
+    const int lds = std::max(NW * (UNITS + UNITS / 16) * 16 + 16 * MT * 4 + 16, MT >= 4 ? NW * MT * 2048 : 0);
     auto kern = skinny_kernel<RT, MT, D, NW, MODE, NORMP>;
     static bool attr = false;
     if (!attr) {
