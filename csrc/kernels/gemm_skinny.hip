@@ -159,6 +159,8 @@ __global__ void __launch_bounds__(64 * NW) skinny_kernel(PPArgs a) {
         }
     }
 
+    // XL: the reduction slots, inv and the flag alias the other waves' x tiles — wait until every wave's loop is done
+    if constexpr (XL) __syncthreads();
     // NORMP: inv[m] of the x rows from the producer's partials — fetched only now, so these loads never sit in front
     // of the weight ring in the in-order vmcnt queue
     if constexpr (NORMP) {
@@ -189,7 +191,6 @@ __global__ void __launch_bounds__(64 * NW) skinny_kernel(PPArgs a) {
     // Slots are padded by one per 16 (v + v/16): the lane-consecutive writes (unit stride CPR) and the
     // thread-consecutive reads (unit stride 1) both hit distinct banks.
     auto red_at = [&](int w, int p, int v) { return w * SZ + p * NP + v + (v >> 4); };
-    if constexpr (XL) __syncthreads();  // the slots alias the other waves' x tiles: every wave's main loop is done
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt)
 #pragma unroll

@@ -93,6 +93,22 @@ def test_swiglu_normp(cfg, splitk):
 
 
 @pytest.mark.parametrize("cfg", sorted(CFGS))
+def test_plain_normp_every_config(cfg):
+    """Folded-norm prologue on every config (odd RT included): with many waves and a long K the first waves to finish
+    write the norm scales while others still stream x through their LDS tiles (the XL configs alias the two)."""
+    rt, mt, nw = CFGS[cfg]
+    g = torch.Generator(device=DEV).manual_seed(90 + cfg)
+    m, n, k = 16 * mt - 5, 16 * rt * 24, 64 * nw * 6
+    s = _rand((m, k), g, 2.0, 0.3)
+    w = _rand((n, k), g, 0.3)
+    sf = s.float()
+    part = torch.stack([(sf[:, i::8] ** 2).sum(1) for i in range(8)], 1).contiguous()
+    inv = torch.rsqrt((sf * sf).sum(1, keepdim=True) / k + 1e-5)
+    y, _ = _sk(s, w, 0, cfg, 1, None, part)
+    _check(y, (sf * inv) @ w.float().t())
+
+
+@pytest.mark.parametrize("cfg", sorted(CFGS))
 @pytest.mark.parametrize("splitk", [1, 4])
 def test_resid_partials(cfg, splitk):
     rt, mt, nw = CFGS[cfg]
