@@ -32,6 +32,7 @@ namespace chronos {
 namespace {
 
 enum : int { kPlain = kPPPlain, kSwiglu = kPPSwiglu, kResid = kPPResid };
+constexpr int XL_MIN_MT = 2;  // x staged through LDS from MT = 2 (x bytes >= the weight bytes per wave)
 
 template <int RT, int MT, int D, int NW, int MODE, bool NORMP>
 __global__ void __launch_bounds__(64 * NW) skinny_kernel(PPArgs a) {
@@ -68,12 +69,12 @@ __global__ void __launch_bounds__(64 * NW) skinny_kernel(PPArgs a) {
             row = g * 16 * RT + 16 * rt;
         wp[rt] = reinterpret_cast<const bf16x8*>(a.w + (int64_t)(row + (lane & 15)) * K + kbase);
     }
-    // XL (MT >= 4, x bytes = MT / RT x the weight bytes): x is loaded in whole 128-B lines (lane l: row 8 i + l / 8,
+    // XL (MT >= XL_MIN_MT, x bytes = MT / RT x the weight bytes): x is loaded in whole 128-B lines (lane l: row 8 i + l / 8,
     // 16-B chunk l % 8 of the unit's 64 k) and turned into the MFMA B layout through the wave's private LDS tile
     // (swizzled ds_write_b128, ds_read_b128).  Loads shaped like the MFMA operand (16 rows x 64 B per instruction)
     // reach only ~18 B/clk per CU from L2 against ~50 for whole lines (csrc/microbench/l2_feed.hip): at M = 128 the x
     // re-reads, not the weight stream, set the kernel time.
-    constexpr bool XL = MT >= 4;
+    constexpr bool XL = MT >= XL_MIN_MT;
     const bf16x8* xp[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -304,7 +305,7 @@ template <int RT, int MT, int D, int NW, int MODE, bool NORMP>
 void launch_cfg(const PPArgs& a, hipStream_t st) {
     constexpr int UNITS = RT * MT * 64;
     // the reduction slots (+ inv, flag) alias the XL x tiles, which are dead once the main loop ends
-    const int lds = std::max(NW * (UNITS + UNITS / 16) * 16 + 16 * MT * 4 + 16, MT >= 4 ? NW * MT * 2048 : 0);
+    const int lds = std::max(NW * (UNITS + UNITS / 16) * 16 + 16 * MT * 4 + 16, MT >= XL_MIN_MT ? NW * MT * 2048 : 0);
     auto kern = skinny_kernel<RT, MT, D, NW, MODE, NORMP>;
     static bool attr = false;
     if (!attr) {
