@@ -27,6 +27,13 @@ int gemm_pp_bm(int cfg);  // x rows per tile
 int gemm_pp_bn(int cfg);  // W rows per tile
 bool launch_gemm_pp(int cfg, int mode, bool normp, bool prio, const PPArgs& a, hipStream_t st);
 
+// large-M family (csrc/kernels/gemm_lg.hip): config ids kPPConfigs .. kPPConfigs + kLGConfigs - 1 of the same PPArgs
+// interface; tile = WN W rows x XM x rows, 4 or 8 waves (2 x NWX), kResid partials are [M, N / (WN / 2)]
+constexpr int kLGConfigs = 12;
+int gemm_lg_xm(int cfg);  // x rows per tile
+int gemm_lg_wn(int cfg);  // W rows per tile
+bool launch_gemm_lg(int cfg, int mode, bool normp, const PPArgs& a, hipStream_t st);
+
 // skinny-M family (csrc/kernels/gemm_skinny.hip, M <= 16 * MT): same PPArgs / epilogues; the workgroup owns 16 * RT
 // W rows (swiglu: 8 * RT gate + 8 * RT up), ws holds [groups * splitk, 64 * RT * MT] f32x4 slabs, cnt one ticket per
 // group, kResid partials are [M, N / (16 * RT)]; K % (64 * NW * splitk) == 0

@@ -543,9 +543,12 @@ std::tuple<Tensor, Tensor> gemm_pp(const Tensor& x, const Tensor& w, int64_t mod
     chk_bf16(w, "w");
     const int64_t K = x.size(-1), M = x.numel() / K, N = w.size(0);
     CHK(w.dim() == 2 && w.size(1) == K, "gemm_pp: w must be [N, K]");
-    CHK(cfg >= 0 && cfg < chronos::kPPConfigs, "gemm_pp: cfg");
+    const bool lg = cfg >= chronos::kPPConfigs;  // gemm_lg.hip configs continue the id space
+    CHK((cfg >= 0 && cfg < chronos::kPPConfigs + chronos::kLGConfigs) || (cfg >= 40 && cfg < 64), "gemm_pp: cfg");
     CHK(mode >= 0 && mode <= 2, "gemm_pp: mode");
-    const int BM = chronos::gemm_pp_bm((int)cfg), BN = chronos::gemm_pp_bn((int)cfg);
+    const int BM = lg ? chronos::gemm_lg_xm((int)cfg) : chronos::gemm_pp_bm((int)cfg);
+    const int BN = lg ? chronos::gemm_lg_wn((int)cfg) : chronos::gemm_pp_bn((int)cfg);
+    const int PCOLS = lg ? BN / 2 : BN / 4;  // output columns per RMSNorm partial (kResid)
     CHK(M >= 1 && M < (1LL << 31) / BM && K % 64 == 0 && K <= (1 << 20) && N * K < (1LL << 40), "gemm_pp: size");
     CHK(splitk >= 1 && (K / 64) % splitk == 0, "gemm_pp: splitk must divide K / 64");
     CHK(mode == 0 ? N % 4 == 0 : N % BN == 0, "gemm_pp: N % 4 (plain) / N % BN (swiglu, resid)");
@@ -572,7 +575,7 @@ std::tuple<Tensor, Tensor> gemm_pp(const Tensor& x, const Tensor& w, int64_t mod
         chk_bf16(*resid, "resid");
         CHK(resid->numel() == M * N, "gemm_pp: resid must be [M, N]");
         a.resid = bf(*resid);
-        part_out = at::empty({M, N / (BN / 4)}, x.options().dtype(at::kFloat));
+        part_out = at::empty({M, N / PCOLS}, x.options().dtype(at::kFloat));
         a.part_out = part_out.data_ptr<float>();
     }
     if (part_in.has_value()) {
@@ -588,7 +591,11 @@ std::tuple<Tensor, Tensor> gemm_pp(const Tensor& x, const Tensor& w, int64_t mod
         a.ws = ws.data_ptr<float>();
         a.cnt = split_tickets(x, tiles);
     }
-    CHK(chronos::launch_gemm_pp((int)cfg, (int)mode, part_in.has_value(), prio, a, cur_stream()), "gemm_pp: launch");
+    if (lg) {
+        CHK(!prio && chronos::launch_gemm_lg((int)cfg, (int)mode, part_in.has_value(), a, cur_stream()), "gemm_lg: launch");
+    } else {
+        CHK(chronos::launch_gemm_pp((int)cfg, (int)mode, part_in.has_value(), prio, a, cur_stream()), "gemm_pp: launch");
+    }
     return {y, part_out};
 }
 

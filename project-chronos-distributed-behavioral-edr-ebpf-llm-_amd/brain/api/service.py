@@ -252,7 +252,14 @@ class LockstepService(EngineService):
                 done, _ = self.tpe.step()
             except Exception as e:
                 self._fatal(e)
-                return  # no further step and no stop broadcast: either would mismatch the followers' collectives
+                # no further step and no stop broadcast (either would mismatch the followers' collectives), but the
+                # thread stays up answering: a request submitted after the failure gets its error reply here
+                while not self._stop.is_set():
+                    try:
+                        self._handle(self._q.get(timeout=0.05))
+                    except queue.Empty:
+                        pass
+                return
             self._step_t0 = None
             if busy:
                 METRICS.observe_step(time.perf_counter() - t, self.engine)

@@ -25,6 +25,8 @@ def main():
 
     ops.load()
     n, k, mode = SHAPES[args.op]
+    if n is None:  # square
+        n = k = args.m
     g = torch.Generator(device="cuda").manual_seed(0)
     x = (torch.rand(args.m, k, device="cuda", generator=g) * 2 - 1).to(torch.bfloat16)
     ncopy = max(2, -(-(600 << 20) // (n * k * 2)))

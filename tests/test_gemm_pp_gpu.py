@@ -35,7 +35,8 @@ def _check(y, ref, tol=2e-2):
     assert err <= tol * scale, f"max err {err:.4g} vs max |ref| {scale:.4g}"
 
 
-CFGS = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11]
+LG = [12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23]  # gemm_lg.hip configs (12-19 ring schedule, 20-23 slab schedule)
+CFGS = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11] + LG
 
 
 @pytest.mark.parametrize("cfg", CFGS)
@@ -49,7 +50,7 @@ def test_plain(cfg, m):
     _check(y, x.float() @ w.float().t())
 
 
-@pytest.mark.parametrize("cfg", [0, 3, 5, 8, 11])
+@pytest.mark.parametrize("cfg", [0, 3, 5, 8, 11] + LG)
 def test_n_tail(cfg):
     """N not a multiple of the tile (the 70B TP=8 LM-head shard is N = 16032): the last W tile is partial."""
     g = torch.Generator(device=DEV).manual_seed(21 + cfg)
@@ -60,7 +61,8 @@ def test_n_tail(cfg):
     _check(y, x.float() @ w.float().t())
 
 
-@pytest.mark.parametrize("cfg,splitk", [(0, 2), (1, 4), (3, 2), (2, 5), (4, 2), (5, 4), (7, 2), (8, 2), (9, 4), (10, 2), (11, 5)])
+@pytest.mark.parametrize("cfg,splitk", [(0, 2), (1, 4), (3, 2), (2, 5), (4, 2), (5, 4), (7, 2), (8, 2), (9, 4), (10, 2), (11, 5),
+                                        (12, 2), (13, 4), (14, 5), (15, 2), (16, 2), (17, 4), (18, 5), (19, 2), (20, 2), (21, 4), (22, 5), (23, 2)])
 def test_splitk(cfg, splitk):
     g = torch.Generator(device=DEV).manual_seed(11 + cfg)
     m, n, k = 300, 512, 64 * 20
@@ -72,7 +74,7 @@ def test_splitk(cfg, splitk):
         _check(y, ref)
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 3, 4, 5, 8, 9, 11])
+@pytest.mark.parametrize("cfg", [0, 1, 3, 4, 5, 8, 9, 11] + LG)
 def test_swiglu_normp(cfg):
     g = torch.Generator(device=DEV).manual_seed(3 + cfg)
     m, f, k = 200, 256, 512
@@ -91,7 +93,8 @@ def test_swiglu_normp(cfg):
     _check(y2, hv)
 
 
-@pytest.mark.parametrize("cfg,splitk", [(0, 1), (1, 2), (3, 1), (4, 1), (5, 2), (8, 1), (9, 2), (10, 1)])
+@pytest.mark.parametrize("cfg,splitk", [(0, 1), (1, 2), (3, 1), (4, 1), (5, 2), (8, 1), (9, 2), (10, 1),
+                                        (12, 1), (12, 2), (13, 1), (14, 2), (15, 1), (16, 1), (17, 2), (18, 1), (19, 2), (20, 1), (20, 2), (21, 1), (22, 2), (23, 1)])
 def test_resid_partials(cfg, splitk):
     g = torch.Generator(device=DEV).manual_seed(5 + cfg)
     m, n, k = 259, 512, 768
@@ -108,7 +111,8 @@ def test_resid_partials(cfg, splitk):
 def test_decode_shapes_vs_library():
     """One 8B decode-bucket shape per projection at M = 1024 against hipBLASLt, tight tolerance."""
     g = torch.Generator(device=DEV).manual_seed(1)
-    for n, k, cfg, sk in [(6144, 4096, 1, 1), (4096, 14336, 1, 2), (4096, 4096, 3, 1)]:
+    for n, k, cfg, sk in [(6144, 4096, 1, 1), (4096, 14336, 1, 2), (4096, 4096, 3, 1), (6144, 4096, 12, 1),
+                          (4096, 14336, 12, 4), (4096, 4096, 13, 2), (28672, 4096, 14, 1), (4096, 4096, 15, 1)]:
         x = _rand((1024, k), g)
         w = _rand((n, k), g, 0.05)
         y, _ = _pp(x, w, 0, cfg, sk)

@@ -118,9 +118,12 @@ def _fail_worker(rank, world, port, q):
     orig, calls = tpe.engine.step, [0]
 
     def bad_step():
-        calls[0] += 1
-        if calls[0] == 2:
-            raise RuntimeError("injected leader-only fault")
+        # count only steps with work: the scheduler also steps while idle (the followers' heartbeat), and a fault
+        # on an idle step would race the first submission
+        if tpe.engine.has_work():
+            calls[0] += 1
+            if calls[0] == 2:
+                raise RuntimeError("injected leader-only fault")
         return orig()
 
     tpe.engine.step = bad_step
@@ -128,8 +131,8 @@ def _fail_worker(rank, world, port, q):
                        format=VERDICT_SCHEMA, num_predict=24)
 
     async def go():
-        r1 = await svc.generate(p)
-        r2 = await asyncio.wait_for(svc.generate(p), 5.0)
+        r1 = await asyncio.wait_for(svc.generate(p), 120.0)
+        r2 = await asyncio.wait_for(svc.generate(p), 30.0)  # after the failure: answered, never left queued
         return r1, r2
 
     r1, r2 = asyncio.run(go())
