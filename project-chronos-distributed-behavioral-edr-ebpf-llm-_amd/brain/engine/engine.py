@@ -167,6 +167,7 @@ class _Snapshot:
     nout: torch.Tensor
     out: torch.Tensor
     owners: dict
+    seq: int = 0  # order in which snapshots were queued (a jump applied after snapshot k makes k's parked rows stale)
 
 
 class Engine:
@@ -266,6 +267,7 @@ class Engine:
         self._snap_bufs = [tuple(torch.zeros(shape, dtype=torch.int32, pin_memory=pin)
                                  for shape in ((S,), (S,), (S, cfg.max_out))) for _ in range(2)]
         self._snap_i = 0
+        self._snap_seq = 0
         self._pending: Optional[_Snapshot] = None
         self._deferred: list = []  # (request, reason) harvested, finished after the next launch (_flush_deferred)
         self._async = cfg.async_harvest
@@ -350,8 +352,10 @@ class Engine:
         if self.running:
             if self._check_parked:
                 # the last sampler launch (prefill / jump) may have parked every row: look before launching a burst
-                # that would then run fully gated
+                # that would then run fully gated.  The fresh snapshot supersedes a mixed step's pending one (device
+                # state only moves forward until a harvest resets it), whose pinned buffer the next snapshot reuses
                 self._check_parked = False
+                self._pending = None
                 with trace.range("harvest"):
                     return reaped + self._harvest(self._snapshot(min(self._decode_rows(), self.cfg.max_slots)))
             with trace.range("decode_burst"):
@@ -752,7 +756,11 @@ class Engine:
 
     def _snapshot(self, n: int) -> _Snapshot:
         st, no, out = self._snap_bufs[self._snap_i]
+        # two alternating pinned buffers: at most ONE snapshot (the pending one) may be outstanding when a new one is
+        # queued, and never in the buffer about to be overwritten
+        assert self._pending is None or self._pending.state is not st, "snapshot buffer still referenced"
         self._snap_i ^= 1
+        self._snap_seq += 1
         st[:n].copy_(self.s_state[:n], non_blocking=True)
         no[:n].copy_(self.s_nout[:n], non_blocking=True)
         out[:n].copy_(self.s_out[:n], non_blocking=True)
@@ -760,7 +768,7 @@ class Engine:
         if self.device.type == "cuda":
             ev = torch.cuda.Event()
             ev.record()
-        return _Snapshot(n, ev, st, no, out, dict(self.running))
+        return _Snapshot(n, ev, st, no, out, dict(self.running), self._snap_seq)
 
     def _gate(self, n: int) -> None:
         """Arm the decode early-exit gate for a small bucket (n <= 8 rows): the steps of a burst after every row's
@@ -803,7 +811,9 @@ class Engine:
         st = snap.state[:snap.n].tolist()
         nout, outs = snap.nout, snap.out
         finished = [(s, r) for s, r in live if st[s] == DONE]
-        parked = [(s, r) for s, r in live if st[s] <= -2]
+        # a parked row whose jump was already applied after this snapshot was queued (a mixed step harvests one step
+        # late) is stale: applying its run again would rewind the row and duplicate the run
+        parked = [(s, r) for s, r in live if st[s] <= -2 and r.meta.get("jump_seq", 0) < snap.seq]
         ended = {}  # slot -> output ids of jumped runs that end the verdict
         if parked:
             t = time.perf_counter()
@@ -886,6 +896,7 @@ class Engine:
                 continue
             ids = outs[s, :n0].tolist() + list(run)
             r.meta.setdefault("jump_spans", []).append((n0, k))
+            r.meta["jump_seq"] = self._snap_seq  # every snapshot queued so far predates this jump
             self.stats["jumps"] += 1
             self.stats["jump_tokens"] += k
             if end == DONE:

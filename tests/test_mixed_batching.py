@@ -100,3 +100,51 @@ def test_wave_backlog_prefills_in_full_steps():
             seen.append(backlog)
     assert seen and max(seen) <= 4
     assert all(r.done_reason in ("stop", "length") for r in reqs)
+
+
+def test_mixed_steps_with_jump_forward_apply_each_run_once():
+    """Jump-forward parking together with mixed steps: a mixed step harvests the snapshot of the step
+    before, which can still show a row parked whose run the previous harvest already appended.  Every run must be
+    applied exactly once (spans strictly increasing, never overlapping) and the output must still be the greedy
+    choice of a fresh forward at every position (teacher forcing)."""
+    import os
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_jump_forward import _teacher_forced_ok
+
+    from chronos.sensor.prompt import VERDICT_SCHEMA
+
+    prompts = _chains(16, seed=9)
+    eng = _engine(mixed_batching=True, jump_forward=True, mixed_prefill_tokens=48, mixed_ratio=1, decode_burst=1)
+    reqs = [eng.submit(p, fmt=VERDICT_SCHEMA, num_predict=40) for p in prompts[:3]]
+    nxt, it, stale = 3, 0, 0
+    harvest = eng._harvest
+
+    def counting_harvest(snap):  # count parked rows a lagging (mixed-step) harvest must skip
+        nonlocal stale
+        st = snap.state[:snap.n].tolist()
+        stale += sum(1 for s, r in snap.owners.items() if eng.running.get(r.slot) is r and st[s] <= -2
+                     and r.meta.get("jump_seq", 0) >= snap.seq)
+        return harvest(snap)
+
+    eng._harvest = counting_harvest
+    # park in mixed steps too (production passes None there): every parked row is then seen by two lagging harvests
+    sample = eng._sample
+    eng._sample = lambda logits, jump: sample(logits, eng._jump_flags(len(eng.running) + 1))
+    while eng.has_work() or nxt < len(prompts):
+        # phases: a few plain decode steps (rows get parked by the decode sampler, jumps resample and park again),
+        # then arrivals every step (mixed steps, whose harvests lag one step behind those parks)
+        if nxt < len(prompts) and eng.running and it % 6 >= 3:
+            reqs.append(eng.submit(prompts[nxt], fmt=VERDICT_SCHEMA, num_predict=40))
+            nxt += 1
+        eng.step()
+        it += 1
+    assert eng.stats["mixed_steps"] > 0 and eng.stats["jumps"] > 0
+    assert stale > 0  # the lagging-harvest case was exercised
+    for r in reqs:
+        assert r.done_reason in ("stop", "length")
+        spans = r.meta.get("jump_spans", [])
+        for (a0, k0), (a1, _) in zip(spans, spans[1:]):
+            assert a1 >= a0 + k0, spans  # a run applied twice would restart at (or before) its own start
+        _teacher_forced_ok(eng, r)
