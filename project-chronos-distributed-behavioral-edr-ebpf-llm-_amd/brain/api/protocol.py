@@ -150,6 +150,23 @@ def apply_stop(text: str, stop: tuple) -> tuple[str, bool]:
     return (text[:cut], True) if cut >= 0 else (text, False)
 
 
+def stop_context_ids(tok, prompt_ids, out_ids, visible: str) -> list:
+    """The continuation ``context`` of a reply cut at a stop string: the prompt, the generated tokens that lie wholly
+    inside the text the client received, then the re-tokenised remainder of that text — never the stop string or
+    what followed it (a continuation must not condition on text the client never saw)."""
+    table = tok.token_bytes_list()
+    vb = visible.encode("utf-8")
+    pos, k = 0, 0
+    for t in out_ids:
+        b = table[t] if 0 <= t < len(table) else b""
+        if not b or not vb.startswith(b, pos):
+            break
+        pos += len(b)
+        k += 1
+    rest = vb[pos:].decode("utf-8", errors="ignore")
+    return [int(t) for t in list(prompt_ids) + list(out_ids[:k])] + ([int(t) for t in tok.encode(rest)] if rest else [])
+
+
 def chat_response(model: str, req) -> dict:
     d = {"model": model, "created_at": now_iso(), "message": {"role": "assistant", "content": req.text}}
     d.update(final_fields(req))

@@ -25,6 +25,7 @@ from aiohttp import web
 
 from ...utils.metrics import METRICS
 from .protocol import (OLLAMA_VERSION, BadRequest, GenerateParams, StopFilter, apply_stop, chat_response,
+                       stop_context_ids,
                        final_fields, generate_response, now_iso)
 
 log = logging.getLogger("chronos.api")
@@ -56,11 +57,20 @@ def make_app(backend, model_name: str = "llama3", request_timeout: float | None 
                 # a request the engine rejected is the client's fault (400); a failed engine step is ours (500)
                 internal = (getattr(req, "meta", None) or {}).get("internal_error", False)
                 return web.json_response({"error": req.error}, status=500 if internal else 400)
+            ctx = None
             if params.stop:  # checked on the finished text: cut at the first stop string, reason "stop"
                 req.text, hit = apply_stop(req.text, params.stop)
                 if hit:
                     req.done_reason = "stop"
-            return web.json_response(chat_response(model, req) if chat else generate_response(model, req, params.ignored))
+                    tok = getattr(backend, "tok", None)
+                    if tok is not None and not chat:
+                        ctx = stop_context_ids(tok, req.prompt_ids, req.out_ids, req.text)
+            if chat:
+                return web.json_response(chat_response(model, req))
+            body = generate_response(model, req, params.ignored)
+            if ctx is not None:
+                body["context"] = ctx
+            return web.json_response(body)
         resp = web.StreamResponse(headers={"Content-Type": "application/x-ndjson"})
         await resp.prepare(request)
         sf = StopFilter(params.stop) if params.stop else None

@@ -43,6 +43,10 @@ class EngineService:
         self._thread.start()
         self._watchdog.start()
 
+    @property
+    def tok(self):
+        return self.engine.tok
+
     @classmethod
     def from_config(cls, cfg: EngineConfig, model_name: str = "llama3") -> "EngineService":
         return cls(Engine(cfg), model_name)

@@ -12,12 +12,19 @@ reference's ERROR verdict path (chronos_sensor.py:121-122) instead of a hang unt
 leaves the routing set, and a FRESH worker process is spawned in its place (never an exec of a process that touched
 the GPU); it rejoins routing when its engine reports ready.  ``/healthz`` shows the transition: "degraded" (503 only
 while no replica is serving) with the dead / restarting replicas and the restart counts.
+
+Respawns are bounded: a worker that dies before reporting ready (OOM at model build, a GPU that fails to initialise)
+is a start-up failure; consecutive ones are respawned after an exponential delay (``respawn_base_s`` doubling, capped
+at ``respawn_cap_s``), and after ``max_start_failures`` in a row the replica is marked failed and never respawned
+(``failed_replicas`` in ``/healthz``) instead of initialising a GPU every poll forever.  A death after ready resets
+the count (the replica had been serving).
 """
 from __future__ import annotations
 
 import asyncio
 import itertools
 import multiprocessing as mp
+import os
 import queue
 import threading
 import time
@@ -27,6 +34,8 @@ from typing import AsyncIterator, Optional
 
 
 def _worker(rank: int, cfg_dict: dict, req_q, res_q, device: str) -> None:
+    if os.environ.get("CHRONOS_FAULT_START_RANK") == str(rank):  # fault injection (tests): die before ready
+        raise SystemExit(7)
     import torch
 
     from ..brain.api.protocol import GenerateParams, chat_prompt_ids
@@ -86,22 +95,40 @@ def _worker(rank: int, cfg_dict: dict, req_q, res_q, device: str) -> None:
 
 class DPRouter:
     def __init__(self, cfg, replicas: int, device: str | None = None, start_timeout: float = 900.0,
-                 respawn: bool = True, poll_s: float = 0.1):
+                 respawn: bool = True, poll_s: float = 0.1, respawn_base_s: float = 1.0, respawn_cap_s: float = 60.0,
+                 max_start_failures: int = 5):
         self.n = replicas
         self._dev = device or ("cuda" if str(cfg.device).startswith("cuda") else "cpu")
         self._ctx = mp.get_context("spawn")
         self._cfgd = asdict(cfg)
         self._res = self._ctx.Queue()
         self._reqs = [self._ctx.Queue() for _ in range(replicas)]
+        self._ready_seen = [False] * replicas  # the current process of each replica reported ready
         self._procs = [self._spawn(r) for r in range(replicas)]
-        ready = 0
         t0 = time.time()
-        while ready < replicas:
-            kind, _, _ = self._res.get(timeout=max(1.0, start_timeout - (time.time() - t0)))
-            ready += kind == "ready"
+        # every replica ready, or dead before ready (the supervisor then owns its respawn / failure); none ready = error
+        while not all(self._ready_seen[r] or not self._procs[r].is_alive() for r in range(replicas)):
+            if time.time() - t0 > start_timeout:
+                raise TimeoutError(f"replicas not ready after {start_timeout:.0f}s")
+            try:
+                kind, rank, _ = self._res.get(timeout=0.5)
+            except queue.Empty:
+                continue
+            if kind == "ready":
+                self._ready_seen[rank] = True
+        if not any(self._ready_seen):
+            codes = [p.exitcode for p in self._procs]
+            for p in self._procs:
+                p.join(timeout=5)
+            raise RuntimeError(f"no replica started (exit codes {codes})")
         self.outstanding = [0] * replicas
-        self.alive = [True] * replicas       # in the routing set
+        self.alive = list(self._ready_seen)  # in the routing set
         self.restarts = [0] * replicas
+        self.start_failures = [0] * replicas  # consecutive deaths before ready
+        self.failed = [False] * replicas      # given up on: never respawned again
+        self._respawn_at: list = [None] * replicas
+        self.respawn_base_s, self.respawn_cap_s = respawn_base_s, respawn_cap_s
+        self.max_start_failures = max_start_failures
         self.failed_requests = 0
         self.respawn = respawn
         self._closing = False
@@ -116,6 +143,7 @@ class DPRouter:
         self._supervisor.start()
 
     def _spawn(self, r: int):
+        self._ready_seen[r] = False
         p = self._ctx.Process(target=_worker, args=(r, self._cfgd, self._reqs[r], self._res, self._dev), daemon=True)
         p.start()
         return p
@@ -129,6 +157,8 @@ class DPRouter:
             if kind == "ready":  # a respawned replica rejoins the routing set
                 with self._lock:
                     self.alive[rid] = True
+                    self._ready_seen[rid] = True
+                    self.start_failures[rid] = 0
                 continue
             with self._lock:
                 w = self._waiters.get(rid)
@@ -153,9 +183,17 @@ class DPRouter:
                 p = self._procs[r]
                 if self._closing or p.is_alive():
                     continue
-                if self._handled[r] is p:  # this death was already handled (respawn off)
+                if self._handled[r] is p:  # this death was already handled: a delayed respawn may be due
+                    due = self._respawn_at[r]
+                    if due is not None and time.time() >= due and not self._closing:
+                        self._respawn_at[r] = None
+                        self._reqs[r] = self._ctx.Queue()  # whatever the dead worker left queued was answered
+                        self._procs[r] = self._spawn(r)
+                        self.restarts[r] += 1
                     continue
                 self._handled[r] = p
+                if not self._ready_seen[r]:
+                    self.start_failures[r] += 1
                 with self._lock:
                     self.alive[r] = False
                     lost = [(rid, w) for rid, w in self._waiters.items() if w[2] == r]
@@ -167,9 +205,12 @@ class DPRouter:
                 for _, (loop, sink, _) in lost:  # answer at once: never leave a caller waiting for a dead replica
                     loop.call_soon_threadsafe(sink, "done", self._error_result(r, f"replica {r} exited ({code})"))
                 if self.respawn and not self._closing:
-                    self._reqs[r] = self._ctx.Queue()  # whatever the dead worker left queued is answered above
-                    self._procs[r] = self._spawn(r)
-                    self.restarts[r] += 1
+                    sf = self.start_failures[r]
+                    if sf >= self.max_start_failures:
+                        self.failed[r] = True  # keeps dying before ready: stop initialising a GPU every poll
+                    else:  # the first respawn after a serving replica died is immediate, start-up failures back off
+                        delay = 0.0 if sf == 0 else min(self.respawn_base_s * 2 ** (sf - 1), self.respawn_cap_s)
+                        self._respawn_at[r] = time.time() + delay
 
     def _dispatch(self, params, stream: bool, sink) -> tuple[int, int]:
         loop = asyncio.get_running_loop()
@@ -182,10 +223,11 @@ class DPRouter:
                 r = min(live, key=lambda i: self.outstanding[i])
                 self.outstanding[r] += 1
                 self._waiters[rid] = (loop, sink, r)
+                # queued under the lock: the supervisor cannot fail this request over and replace the queue in between
+                # (the respawned worker would then run a request whose caller already got its error reply)
+                self._reqs[r].put((rid, asdict(params), stream))
         if r < 0:  # every replica is down or restarting: the error verdict now, not a hang
             loop.call_soon(sink, "done", self._error_result(-1, "no replica available (restarting)"))
-            return rid, r
-        self._reqs[r].put((rid, asdict(params), stream))
         return rid, r
 
     def _cancel(self, rid: int, r: int) -> None:
@@ -201,6 +243,14 @@ class DPRouter:
             if isinstance(v[key], int):
                 v[key] = [0] * v[key]
         return SimpleNamespace(**v)
+
+    @property
+    def tok(self):
+        if getattr(self, "_tok", None) is None:
+            from ..brain.tokenizer import load_tokenizer
+
+            self._tok = load_tokenizer(None)
+        return self._tok
 
     async def generate(self, params):
         fut = asyncio.get_running_loop().create_future()
@@ -219,10 +269,7 @@ class DPRouter:
     async def generate_stream(self, params) -> AsyncIterator[tuple[str, Optional[object]]]:
         aq: asyncio.Queue = asyncio.Queue()
         rid, r = self._dispatch(params, True, lambda kind, val: aq.put_nowait((kind, val)))
-        from ..brain.tokenizer import load_tokenizer
-
-        tok = getattr(self, "_tok", None) or load_tokenizer(None)
-        self._tok = tok
+        tok = self.tok
         finished = False
         try:
             while True:
@@ -244,9 +291,11 @@ class DPRouter:
             serving = [i for i in range(self.n) if self.alive[i] and self._procs[i].is_alive()]
             dead = [i for i in range(self.n) if not self._procs[i].is_alive()]
             restarting = [i for i in range(self.n) if not self.alive[i] and self._procs[i].is_alive()]
+            failed = [i for i in range(self.n) if self.failed[i]]
         status = "ok" if len(serving) == self.n else ("degraded" if serving else "down")
         return bool(serving), {"status": status, "serving_replicas": serving, "dead_replicas": dead,
-                               "restarting_replicas": restarting, "restarts": list(self.restarts),
+                               "restarting_replicas": restarting, "failed_replicas": failed,
+                               "restarts": list(self.restarts), "start_failures": list(self.start_failures),
                                "failed_over_requests": self.failed_requests}
 
     def info(self) -> dict:

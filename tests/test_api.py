@@ -281,6 +281,13 @@ def test_ollama_options_stop_num_ctx_context(tiny_service):
     cut = requests.post(url, json=dict(base, options={"num_predict": 48, "stop": ['"verdict"']}), timeout=60).json()
     assert cut["response"] == full["response"][:full["response"].index('"verdict"')]
     assert cut["done_reason"] == "stop"
+    # the continuation context ends where the visible text ends: the stop string and what followed are not in it
+    from chronos.brain.tokenizer import load_tokenizer
+
+    tok = load_tokenizer(None)
+    gen_ctx = cut["context"][cut["prompt_eval_count"]:]
+    assert tok.decode(gen_ctx) == cut["response"]
+    assert cut["context"][:cut["prompt_eval_count"]] == full["context"][:full["prompt_eval_count"]]
     r = requests.post(url, json=dict(base, stream=True, options={"num_predict": 48, "stop": '"verdict"'}),
                       stream=True, timeout=60)
     lines = [json.loads(l) for l in r.iter_lines() if l]
