@@ -115,6 +115,10 @@ PRESETS: dict[str, LlamaConfig] = {
                         num_kv_heads=2, max_position=4096),
     "small": LlamaConfig(name="small", hidden_size=1024, intermediate_size=2816, num_layers=4, num_heads=8,
                          num_kv_heads=2, max_position=8192),
+    # the 70B attention geometry (64 q / 8 KV heads: at TP=8 one KV head per rank, GQA group 8) and the real vocab
+    # (a 16032-row shard per rank at TP=8, not a multiple of 128) in a CPU-sized model (hidden 256, 2 layers)
+    "tiny70": LlamaConfig(name="tiny70", hidden_size=256, intermediate_size=512, num_layers=2, num_heads=64,
+                          num_kv_heads=8, max_position=4096),
 }
 
 

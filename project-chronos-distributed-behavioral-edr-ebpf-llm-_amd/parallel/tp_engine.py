@@ -52,16 +52,17 @@ class TPEngine:
     """Lockstep replicated scheduler over a TP group — or, with ``cp``, over a context-parallel group of full-weight
     ranks (parallel/context_parallel.py); the control plane is the same."""
 
-    def __init__(self, cfg: EngineConfig, tp: TPContext, ctrl_group=None, cp: TPContext | None = None):
+    def __init__(self, cfg: EngineConfig, tp: TPContext, ctrl_group=None, cp: TPContext | None = None, model=None):
+        """``model``: a prebuilt (already sharded) model for this rank instead of ``cfg.model`` (tests: fp32 weights)."""
         from dataclasses import replace
 
         self.tp = tp if cp is None else cp  # the lockstep group
         self.ctrl = ctrl_group  # gloo group spanning the lockstep ranks (host-side control plane)
         self.timeout_s = cfg.request_timeout_s  # enforced by the leader only (module docstring)
         if cp is None:
-            self.engine = Engine(replace(cfg, request_timeout_s=0.0), tp=tp)
+            self.engine = Engine(replace(cfg, request_timeout_s=0.0), tp=tp, model=model)
         else:
-            self.engine = Engine(replace(cfg, request_timeout_s=0.0), cp=cp)
+            self.engine = Engine(replace(cfg, request_timeout_s=0.0), cp=cp, model=model)
         self.leader = self.tp.rank == 0
         self._inbox: "queue.Queue[_Sub]" = queue.Queue()
         self._cancel_inbox: "queue.Queue[tuple[int, str]]" = queue.Queue()

@@ -47,8 +47,9 @@ def test_bench_two_ranks(tp, sp):
 
 
 def _run_plain(gpus_args, env_extra=None, timeout=600):
+    model = "tiny70" if "--tp" in gpus_args else "tiny"
     cmd = [sys.executable, os.path.join(REPO, "bench.py")] + gpus_args + [
-        "--device", "cpu", "--model", "tiny", "--streams", "3", "--steps", "1", "--warmup", "1",
+        "--device", "cpu", "--model", model, "--streams", "3", "--steps", "1", "--warmup", "1",
         "--num-predict", "24", "--single-stream", "2", "--no-graphs", "--max-model-len", "384"]
     env = dict(os.environ, OMP_NUM_THREADS="2", **(env_extra or {}))
     env.pop("WORLD_SIZE", None) if not env_extra or "WORLD_SIZE" not in env_extra else None
@@ -70,3 +71,16 @@ def test_bench_gpus_flag_self_launches():
 def test_bench_gpus_mismatch_is_an_error():
     out = _run_plain(["--gpus", "2"], {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"}, timeout=300)
     assert out.returncode != 0 and "disagrees with WORLD_SIZE" in out.stderr
+
+
+@pytest.mark.slow
+def test_bench_tp8_70b_geometry_self_launch():
+    """The 70B TP=8 serving shape at its real degree: `bench.py --gpus 8 --tp 8` on the tiny70 preset (64 q / 8 KV
+    heads: one KV head per rank; 16032-row vocab shards), 8 gloo ranks in one lockstep TP group."""
+    out = _run_plain(["--gpus", "8", "--tp", "8"], timeout=900)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    r = json.loads(lines[0])
+    assert r["n_gpus"] == 8 and r["config"]["parallelism"] == "tp8" and r["config"]["model"] == "tiny70"
+    assert r["verdicts_valid"] == "3/3" and "TP=8" in r["metric"]

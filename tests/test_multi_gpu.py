@@ -61,6 +61,18 @@ def _cfg(device):
                         decode_burst=4, seed=0)
 
 
+PROMPTS = [[128000] + list(range(10, 47)), list(range(200, 219)), list(range(300, 305))]
+
+
+def _first_logits(model, device):
+    """fp32 logits of one 3-prompt prefill step (the first decode step's input distribution), on the host."""
+    from chronos.models.llama import KVCache, make_prefill_batch
+
+    kv = KVCache(model.cfg, model.tp, 12, 16, device)
+    sb = make_prefill_batch(PROMPTS, [0, 0, 0], [[1, 2, 3], [4, 5], [6]], model.cfg, model.tp, device, max_blocks=3)
+    return model.forward(sb, kv, logits_dtype=torch.float32).float().cpu().numpy()
+
+
 def _tp_worker(rank, world, port, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
@@ -75,6 +87,7 @@ def _tp_worker(rank, world, port, q):
         tp, ctrl = init_tp("nccl")
         res["ipc"] = getattr(tp, "ipc_allreduce", None) is not None
         eng = TPEngine(_cfg(f"cuda:{rank}"), tp, ctrl_group=ctrl)
+        res["logits"] = _first_logits(eng.engine.model, f"cuda:{rank}")  # every rank: the forward is collective
         if rank == 0:
             out = {}
             for i, c in enumerate(CHAINS):
@@ -102,6 +115,7 @@ def test_tp_engine_distinct_gpus_matches_tp1(world):
     from chronos.sensor.prompt import VERDICT_SCHEMA, build_prompt
 
     ref = Engine(_cfg("cuda:0"))
+    ref_logits = torch.from_numpy(_first_logits(ref.model, "cuda:0"))
     reqs = [ref.submit(build_prompt(c), fmt=VERDICT_SCHEMA, num_predict=40) for c in CHAINS]
     ref.run_until_idle()
     want = [list(r.out_ids) for r in reqs]
@@ -110,6 +124,12 @@ def test_tp_engine_distinct_gpus_matches_tp1(world):
     got = _spawn(_tp_worker, world, timeout=400)
     assert all(got.get(r, {}).get("ok") for r in range(world)), got
     assert all(got[r]["ipc"] for r in range(world)), "IPC all-reduce fell back to RCCL on a peer-capable node"
+    # a systematic sharding error that still emits valid JSON fails here: bf16 logits within 2 % of max |logit|
+    # (the whole-model numerics tolerance, test_model_numerics_gpu.py) and the same argmax on every prompt
+    for r in range(world):
+        lg = torch.from_numpy(got[r]["logits"])
+        assert (lg - ref_logits).abs().max() <= 0.02 * ref_logits.abs().max(), r
+        assert (lg.argmax(-1) == ref_logits.argmax(-1)).all(), r
     out = got[0]["out"]
     agree = 0.0
     for i, w in enumerate(want):
@@ -186,6 +206,8 @@ def test_cp_prefill_distinct_gpus(mode):
     assert all(got.get(r, {}).get("ok") for r in range(2)), got
     assert got[0]["out"] == got[1]["out"] and got[0]["cp_steps"] >= 1  # lockstep: every rank, the same verdict
     assert set(json.loads(got[0]["text"])) == {"risk_score", "verdict", "reason"}
+    # the first token comes straight from the CP prefill's logits: a wrong K/V exchange changes it
+    assert got[0]["out"][:1] == want[:1]
     # GEMMs over other row subsets round differently: greedy paths agree on a prefix, as in the TP test above
     n = min(len(want), len(got[0]["out"]))
     assert sum(a == b for a, b in zip(got[0]["out"][:n], want[:n])) / max(1, n) > 0.5
