@@ -65,7 +65,7 @@ def parse():
     ap.add_argument("--no-mixed", action="store_true",
                     help="separate prefill steps (no prefill chunks riding in the decode batch's forward)")
     ap.add_argument("--mode", choices=["wave", "closed"], default="wave")
-    ap.add_argument("--closed-steps", type=int, default=2,
+    ap.add_argument("--closed-steps", type=int, default=6,
                     help="wave mode: afterwards also time this many closed-loop steps (steady-state arrivals) and "
                          "report them as closed_loop_* next to the headline (0 = skip)")
     ap.add_argument("--weights", choices=["bf16", "fp8"], default="bf16",
@@ -80,8 +80,9 @@ def parse():
     return ap.parse_args()
 
 
-def run_closed(a, eng, prompts, barrier, progress, steps=None, warmup=None):
-    """Steady state: each stream resubmits on completion.  Returns (elapsed, timed requests, prefix-hit tokens)."""
+def run_closed(a, eng, prompts, barrier, progress, steps=None, warmup=None, step_times=None):
+    """Steady state: each stream resubmits on completion.  Returns (elapsed, timed requests, prefix-hit tokens);
+    ``step_times`` (a list) receives the wall time of every block of --streams completions (the step-to-step spread)."""
     from chronos.sensor.prompt import VERDICT_SCHEMA
 
     steps = a.steps if steps is None else steps
@@ -112,8 +113,13 @@ def run_closed(a, eng, prompts, barrier, progress, steps=None, warmup=None):
     n0, hit0 = len(done), eng.stats["prefix_hit_tokens"]
     t0 = time.perf_counter()
     target = n0 + steps * a.streams
+    mark, t_mark = n0 + a.streams, t0
     while len(done) < target and eng.has_work():
         eng.step()
+        if step_times is not None and len(done) >= mark:
+            now = time.perf_counter()
+            step_times.append(now - t_mark)
+            mark, t_mark = mark + a.streams, now
     barrier()
     elapsed = time.perf_counter() - t0
     hits = eng.stats["prefix_hit_tokens"] - hit0
@@ -201,7 +207,8 @@ def main():
     eng = Engine(cfg, tp=tp)
     total_steps = a.warmup + a.steps
     per_stream = total_steps if a.mode == "wave" else 2 * total_steps + 2  # closed loop: fast streams cycle more
-    closed_per = 2 * (1 + a.closed_steps) + 2 if a.mode == "wave" and a.closed_steps > 0 else 0
+    closed_warm = 2  # closed-loop warmup steps (the prefix cache and decode buckets settle)
+    closed_per = 2 * (closed_warm + a.closed_steps) + 2 if a.mode == "wave" and a.closed_steps > 0 else 0
     chains = synthetic_chains(a.streams * (per_stream + closed_per) + a.single_stream, seed=1000 + replica)
     prompts = [build_prompt(c.history) for c in chains]
     n_main, n_closed = a.streams * per_stream, a.streams * closed_per
@@ -261,10 +268,12 @@ def main():
     closed = None
     if closed_per:  # steady-state arrivals after the wave headline
         eng.blocks.clear_cache()
+        c_steps: list = []
         c_el, c_timed, _ = run_closed(a, eng, prompts[n_main:n_main + n_closed], barrier, progress,
-                                      steps=a.closed_steps, warmup=1)
-        closed = dict(elapsed=c_el, n=len(c_timed), lat=[r.latency for r in c_timed])
-        progress(f"closed loop: {len(c_timed)} chains in {c_el:.2f}s")
+                                      steps=a.closed_steps, warmup=closed_warm, step_times=c_steps)
+        closed = dict(elapsed=c_el, n=len(c_timed), lat=[r.latency for r in c_timed], steps=c_steps)
+        progress(f"closed loop: {len(c_timed)} chains in {c_el:.2f}s; per-step s: "
+                 + ", ".join(f"{x:.3f}" for x in c_steps))
 
     # single-stream latency (the reference's regime: one chain in flight)
     single = []
@@ -336,7 +345,13 @@ def main():
             out.update(closed_loop_chains_s=round(sum(s["closed"]["n"] for s in allst) / c_t, 3),
                        closed_loop_p50_ms=round(1000 * statistics.median(c_lat), 2),
                        closed_loop_p99_ms=round(1000 * c_lat[max(0, math.ceil(0.99 * len(c_lat)) - 1)], 2),
-                       closed_loop_steps=a.closed_steps)
+                       closed_loop_steps=a.closed_steps, closed_loop_warmup=closed_warm)
+            cs = allst[0]["closed"]["steps"]  # replica 0's step-to-step spread (chains/s of each --streams block)
+            if cs:
+                rates = [a.streams / x for x in cs]
+                out.update(closed_loop_step_chains_s_min=round(min(rates), 1),
+                           closed_loop_step_chains_s_max=round(max(rates), 1),
+                           closed_loop_step_chains_s_cv=round(statistics.pstdev(rates) / statistics.mean(rates), 4))
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
