@@ -28,11 +28,6 @@ void launch_rmsnorm(const uint16_t*, uint16_t*, const uint16_t*, uint16_t*, int,
 void launch_rope_kv_write(const uint16_t*, const int32_t*, const int32_t*, const int32_t*, int, const float*,
                           uint16_t*, void*, void*, int, int, int, int, int, bool, float, float, hipStream_t);
 void launch_silu_mul(const uint16_t*, uint16_t*, int64_t, int, hipStream_t);
-bool launch_attn_o(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const int32_t* bt,
-                   const int32_t* ctx_len, int hq, int hkv, int block_size, float scale_log2, const uint16_t* w,
-                   const uint16_t* rin, uint16_t* rout, float* part_out, int N, int K, uint16_t* attn_out, int* sync,
-                   int* err, int grid_cap, hipStream_t st);
-int attn_o_parts(int N);
 size_t paged_attn_smem(int nqt);
 bool launch_decode_attn_rope(const uint16_t*, const int32_t*, const float*, void*, void*, const int32_t*, int,
                              const int32_t*, uint16_t*, int, int, int, int, float, hipStream_t);
@@ -478,45 +473,6 @@ Tensor gemm(const Tensor& x, const Tensor& w, bool swiglu, int64_t stages) {
     return y;
 }
 
-// Single-stream decode: attention of the one new token + O projection + residual epilogue in one persistent launch
-// (decode_fused.hip).  Returns (s, part) like gemv_resid, or empty tensors when the fused kernel does not take the
-// shape (the caller then runs paged_attention + gemv_resid).  Scratch (the handed-off attention output, the two
-// counters, the error word) is one buffer per (device, stream), kept zero between launches by the kernel itself.
-std::tuple<Tensor, Tensor> attn_o(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache,
-                                  const Tensor& block_table, const Tensor& ctx_len, const Tensor& w,
-                                  const Tensor& resid, double scale, int64_t grid_cap) {
-    chk_bf16(q, "q");
-    chk_bf16(w, "w");
-    chk_bf16(resid, "resid");
-    const bool fp8 = chk_kv(k_cache, v_cache);
-    chk_i32(block_table, "block_table");
-    chk_i32(ctx_len, "ctx_len");
-    const int64_t hq = q.size(1), hkv = k_cache.size(1), bs = k_cache.size(2), N = w.size(0), K = w.size(1);
-    if (fp8 || q.dim() != 3 || q.size(0) != 1 || q.size(2) != 128 || K != hq * 128 || resid.numel() != N ||
-        bs % 16 || hq % hkv || 16 % (hq / hkv))
-        return {Tensor(), Tensor()};
-    c10::hip::HIPGuardMasqueradingAsCUDA g(q.device());
-    static std::mutex mu;
-    static std::unordered_map<int64_t, Tensor> scratch;
-    int32_t* sp;
-    {
-        std::lock_guard<std::mutex> lk(mu);
-        const int64_t key = ((int64_t)q.get_device() << 48) ^ (int64_t)(intptr_t)cur_stream();
-        auto it = scratch.find(key);
-        // [0, 16) ints: counters + error word; then the attention output (bf16, 8192 max)
-        if (it == scratch.end()) it = scratch.emplace(key, at::zeros({16 + 8192 / 2}, q.options().dtype(at::kInt))).first;
-        sp = it->second.data_ptr<int32_t>();
-    }
-    Tensor s = at::empty_like(resid);
-    Tensor part = at::empty({1, chronos::attn_o_parts((int)N)}, q.options().dtype(at::kFloat));
-    const bool ok = chronos::launch_attn_o(
-        bf(q), reinterpret_cast<const uint16_t*>(k_cache.data_ptr()), reinterpret_cast<const uint16_t*>(v_cache.data_ptr()),
-        i32(block_table), i32(ctx_len), (int)hq, (int)hkv, (int)bs, (float)scale * 1.4426950408889634f, bf(w),
-        bf(resid), bfm(s), part.data_ptr<float>(), (int)N, (int)K, reinterpret_cast<uint16_t*>(sp + 16), sp, sp + 2,
-        (int)grid_cap, cur_stream());
-    if (!ok) return {Tensor(), Tensor()};
-    return {s, part};
-}
 
 // Split-K tickets: one zeroed int buffer per (device, stream), at least n long; every call leaves it zeroed (each
 // group's last arriver resets its own counter), so calls on one stream — and graph replays — share it.
@@ -549,6 +505,8 @@ std::tuple<Tensor, Tensor> gemm_pp(const Tensor& x, const Tensor& w, int64_t mod
     const int BM = lg ? chronos::gemm_lg_xm((int)cfg) : chronos::gemm_pp_bm((int)cfg);
     const int BN = lg ? chronos::gemm_lg_wn((int)cfg) : chronos::gemm_pp_bn((int)cfg);
     const int PCOLS = lg ? BN / 2 : BN / 4;  // output columns per RMSNorm partial (kResid)
+    // gemm_lg addresses both operands through buffer descriptors: 32-bit byte offsets, with one tile of slack
+    CHK(!lg || ((N + BN) * K * 2 < (1LL << 31) && (M + BM) * K * 2 < (1LL << 31)), "gemm_lg: operand > 2 GiB");
     CHK(M >= 1 && M < (1LL << 31) / BM && K % 64 == 0 && K <= (1 << 20) && N * K < (1LL << 40), "gemm_pp: size");
     CHK(splitk >= 1 && (K / 64) % splitk == 0, "gemm_pp: splitk must divide K / 64");
     CHK(mode == 0 ? N % 4 == 0 : N % BN == 0, "gemm_pp: N % 4 (plain) / N % BN (swiglu, resid)");
@@ -777,8 +735,6 @@ TORCH_LIBRARY(chronos, m) {
     m.def("gemm_pp(Tensor x, Tensor w, int mode, int cfg, int splitk, Tensor? resid, Tensor? part_in, float eps, bool prio) -> (Tensor, Tensor)");
     m.def("gemm_skinny(Tensor x, Tensor w, int mode, int cfg, int splitk, Tensor? resid, Tensor? part_in, float eps) "
           "-> (Tensor, Tensor)");
-    m.def("attn_o(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_table, Tensor ctx_len, Tensor w, "
-          "Tensor resid, float scale, int grid_cap) -> (Tensor, Tensor)");
     m.def("gemv_resid(Tensor x, Tensor w, Tensor resid_in, Tensor(a!) resid_out) -> Tensor");
     m.def("gemv_normp(Tensor s, Tensor part, float eps, Tensor w, bool swiglu) -> Tensor");
     m.def("qkv_rope(Tensor x, Tensor? part, float eps, Tensor w, Tensor pos, Tensor tok_seq, "
@@ -818,7 +774,6 @@ TORCH_LIBRARY_IMPL(chronos, CUDA, m) {
     m.impl("gemm", &gemm);
     m.impl("gemm_pp", &gemm_pp);
     m.impl("gemm_skinny", &gemm_skinny);
-    m.impl("attn_o", &attn_o);
     m.impl("gemv_resid", &gemv_resid);
     m.impl("gemv_normp", &gemv_normp);
     m.impl("qkv_rope", &qkv_rope);

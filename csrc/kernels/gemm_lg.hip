@@ -34,6 +34,8 @@
 #include "chronos_hip.h"
 #include "chronos_gemm.h"
 
+#include <type_traits>
+
 namespace chronos {
 namespace {
 
@@ -57,18 +59,31 @@ __device__ __forceinline__ void lg_bar() {
     __builtin_amdgcn_sched_barrier(0);
 }
 
-// compile-time interleave of one MFMA block: MFMA i is followed by its share of the NV DMA pieces and NR ds_reads
-// (T19: sched_group_barrier masks MFMA 0x008, VMEM read 0x020, DS read 0x100)
+// compile-time interleave of one MFMA block (T19: sched_group_barrier masks MFMA 0x008, VMEM 0x010, DS read 0x100):
+// the NV DMA pieces one per MFMA at the head, then the NR ds_reads spread over the remaining MFMAs.  Every DMA goes
+// before every ds_read of the block: an LDS-DMA issued after a ds_read makes hipcc wait for that read (lgkmcnt) first,
+// since it cannot tell the two touch different buffers
+// The last quarter of the block issues no read, so the next block's first MFMAs find their fragments landed.
 template <int I, int MF, int NV, int NR>
 __device__ __forceinline__ void lg_sched() {
     if constexpr (I < MF) {
-        constexpr int v = (I + 1) * NV / MF - I * NV / MF;
-        constexpr int r = (I + 1) * NR / MF - I * NR / MF;
-        if constexpr (v > 0) __builtin_amdgcn_sched_group_barrier(0x020, v, 0);
+        constexpr int R0 = NV < MF ? NV : MF;                   // first MFMA after the DMA head
+        constexpr int R1 = MF - MF / 4 > R0 ? MF - MF / 4 : MF;  // reads spread over MFMAs [R0, R1)
+        constexpr int r = (I < R0 || I >= R1) ? 0 : ((I - R0 + 1) * NR / (R1 - R0) - (I - R0) * NR / (R1 - R0));
+        if constexpr (I < NV) __builtin_amdgcn_sched_group_barrier(0x010, 1, 0);
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         if constexpr (r > 0) __builtin_amdgcn_sched_group_barrier(0x100, r, 0);
         lg_sched<I + 1, MF, NV, NR>();
     }
+}
+
+// One 1 KiB LDS-DMA piece through a buffer descriptor (base / size wave-uniform: kernel arguments): lane l's 16 bytes
+// from byte voff + soff of the buffer to LDS dst + 16 l; bytes past `bytes` read as zeros.  (A descriptor held in
+// a kernel-body variable made hipcc's host pass drop the kernel stubs; built here it is hoisted all the same.)
+__device__ __forceinline__ void lg_dma16(const void* base, int bytes, unsigned char* dst, uint32_t voff, int soff) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, bytes,
+                                                                       0x00020000);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)dst, 16, voff, soff, 0, 0);
 }
 
 // 64-B-row chunk swizzle (the 16x16x32 fragment reads of a 16-row block land on 16 distinct 16-B slots)
@@ -76,7 +91,9 @@ __device__ __forceinline__ int lg_swz64(int row) { return (4 - ((row >> 2) & 3))
 
 // ABL (timing diagnostics only, plain mode): 1 no DMA in the loop, 2 no fragment reads in the loop, 4 no MFMA,
 // 8 every tile's DMA sources aliased onto tile (0, 0) (operands L2-resident)
-template <int WN, int XM, int RB, int ST, int MODE, bool NORMP, int NWX, int ABL = 0>
+// STG (slab schedule, 8 waves): the slab's DMA is split between the wave groups — waves 0-3 issue theirs in k-step B,
+// waves 4-7 (their SIMD partners) in the next k-step A — so one wave of each SIMD issues DMA while the other runs MFMAs
+template <int WN, int XM, int RB, int ST, int MODE, bool NORMP, int NWX, int ABL = 0, bool STG = false>
 __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
     constexpr int NW = 2 * NWX;                       // waves: 2 along W x NWX along x (NWX = 4: two per SIMD)
     constexpr int RPI = 1024 / RB;                    // image rows per LDS-DMA instruction
@@ -93,6 +110,7 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
     // ST == 2: the slab schedule (two 64-deep LDS buffers, fragments pipelined per 32-deep k-step, one barrier per
     // slab); ST >= 3: the ring schedule (DMA of stage t+ST-1 into the buffer of stage t-1)
     constexpr bool SLAB = ST == 2;
+    static_assert(!STG || (SLAB && NWX == 4), "staggered DMA: slab schedule, two waves per SIMD");
     static_assert(ST >= 3 || (SLAB && RB == 128), "slab schedule: 64-deep (128-B row) slabs");
     static_assert(MODE != kSwiglu || (WN / 4) % 16 == 0, "swiglu: WN/4 gate rows per wave, multiple of 16");
     static_assert(RB == 64 || RB == 128, "stage depth 32 or 64");
@@ -124,27 +142,32 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
 
     // ---- LDS-DMA sources: instruction q of the stage (q = wave * NPER + i) fills image rows q*RPI .. +RPI of the
     // concatenated [W rows; x rows] image; lane l fills row q*RPI + l / (RB/16), physical chunk l % (RB/16), from the
-    // logical chunk the read-side swizzle maps there
-    const uint16_t* src[NPER];
+    // logical chunk the read-side swizzle maps there.  buffer_load ... lds through one descriptor per operand: a 32-bit
+    // per-lane byte offset (half the VGPRs of flat 64-bit addresses), the stage's k offset in the scalar soffset, and
+    // rows past the end of W / x (partial last tiles) read as zeros by the descriptor's range check (never stored)
+    const int wbytes = (int)((MODE == kSwiglu ? 2 * a.F : a.N) * (int64_t)K * 2), xbytes = (int)((int64_t)M * K * 2);
+    uint32_t voff[NPER];
     int dsto[NPER];
+    bool isw[NPER];
 #pragma unroll
     for (int i = 0; i < NPER; ++i) {
         const int q = wave * NPER + i;
         const int r = q * RPI + lane / (RB / 16);
         const int pc = lane % (RB / 16);
         dsto[i] = q * 1024;
+        isw[i] = q * RPI < WN;  // wave-uniform
         if (r < WN) {
             int wrow;
             if constexpr (MODE == kSwiglu)
                 wrow = r < WN / 2 ? tns * (WN / 2) + r : a.F + tns * (WN / 2) + (r - WN / 2);
             else
-                wrow = min(tns * WN + r, a.N - 1);  // a partial last W tile re-reads row N-1 (never stored)
+                wrow = tns * WN + r;
             const int lc = RB == 64 ? pc ^ lg_swz64(r) : pc ^ (r & 7);
-            src[i] = a.w + (int64_t)wrow * K + kbeg + lc * 8;
+            voff[i] = (uint32_t)(((int64_t)wrow * K + kbeg + lc * 8) * 2);
         } else {
             const int xr = r - WN;
             const int lc = RB == 64 ? pc ^ lg_swz64(xr) : pc ^ (xr & 7);
-            src[i] = a.x + (int64_t)min(m0s + xr, M - 1) * K + kbeg + lc * 8;
+            voff[i] = (uint32_t)(((int64_t)(m0s + xr) * K + kbeg + lc * 8) * 2);
         }
     }
     // DMA of stage j into ring buffer j % ST.  Issued unconditionally so it shares a basic block with the MFMAs it is
@@ -153,10 +176,10 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
     const int NS1 = NS - 1;
     auto issue = [&](int j) {
         unsigned char* st = smem + (j % ST) * STAGE;
-        const int koff = min(j, NS1) * (RB / 2);
+        const int kb = min(j, NS1) * RB;  // byte offset of stage j in the row
 #pragma unroll
         for (int i = 0; i < NPER; ++i)
-            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(src[i] + koff), (lds_ptr_t)(st + dsto[i]), 16, 0, 0);
+            lg_dma16(isw[i] ? (const void*)a.w : (const void*)a.x, isw[i] ? wbytes : xbytes, st + dsto[i], voff[i], kb);
     };
 
     // ---- fragment addressing: W rows (MFMA A) and x rows (MFMA B); the swizzle term is lane-constant
@@ -196,8 +219,10 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
     }
 
     // ---- prologue: stages 0 .. ST-2 in flight (slab schedule: slabs 0 and 1)
+    const int grp = wave >> 2;  // wave group (STG): waves w and w+4 share a SIMD
 #pragma unroll
-    for (int p = 0; p < (SLAB ? 2 : ST - 1); ++p) issue(p);
+    for (int p = 0; p < (SLAB ? 2 : ST - 1); ++p)
+        if (!(STG && p == 1 && grp == 1)) issue(p);  // (STG: group 1 issues its part of slab 1 in slab 0's k-step A)
 
     if constexpr (NORMP) {
         float* inv = reinterpret_cast<float*>(smem + EXTRA + 16);
@@ -248,9 +273,40 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
             }
         };
         constexpr int MF = NT * MT, NR = NT + MT;
-        lg_vmcnt<NPER>();  // slab 0 landed (slab 1 in flight)
+        if constexpr (STG) {
+            if (grp == 0) lg_vmcnt<NPER>();  // slab 0 landed (group 0's part of slab 1 in flight)
+            else lg_vmcnt<0>();
+        } else {
+            lg_vmcnt<NPER>();  // slab 0 landed (slab 1 in flight)
+        }
         lg_bar();
         rd(0, 0, fa0, fb0);
+        // STG: one straight-line loop per wave group (the DMA sits in a different k-step), so each keeps its
+        // compile-time interleave
+        auto loop_stg = [&](auto G) {
+            constexpr int g = decltype(G)::value;
+            for (int j = 0; j < NS; ++j) {
+                // k-step A (group 1: its part of slab j+1's DMA, into buffer (j+1) % 2, free since barrier j-1)
+                if constexpr (g == 1) issue(j + 1);
+                rd(j, 1, fa1, fb1);
+                mm(fa0, fb0);
+                lg_sched<0, MF, g == 1 ? NPER : 0, NR>();
+                __builtin_amdgcn_sched_barrier(0);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                lg_vmcnt<0>();
+                lg_bar();
+                // k-step B (group 0: its part of slab j+2)
+                if constexpr (g == 0) issue(j + 2);
+                rd(j + 1, 0, fa0, fb0);
+                mm(fa1, fb1);
+                lg_sched<0, MF, g == 0 ? NPER : 0, NR>();
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        };
+        if constexpr (STG) {
+            if (grp == 0) loop_stg(std::integral_constant<int, 0>{});
+            else loop_stg(std::integral_constant<int, 1>{});
+        } else
         for (int j = 0; j < NS; ++j) {
             // k-step A
             if constexpr (!(ABL & 2)) rd(j, 1, fa1, fb1);
@@ -462,10 +518,10 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
     }
 }
 
-template <int WN, int XM, int RB, int ST, int MODE, bool NORMP, int NWX, int ABL = 0>
+template <int WN, int XM, int RB, int ST, int MODE, bool NORMP, int NWX, int ABL = 0, bool STG = false>
 void lg_launch(const PPArgs& a, hipStream_t st) {
     const int lds = ST * (WN + XM) * RB + 16 + XM * 4;
-    auto kern = gemm_lg_kernel<WN, XM, RB, ST, MODE, NORMP, NWX, ABL>;
+    auto kern = gemm_lg_kernel<WN, XM, RB, ST, MODE, NORMP, NWX, ABL, STG>;
     static bool attr = false;
     if (!attr) {
         hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
@@ -490,13 +546,15 @@ void lg_launch(const PPArgs& a, hipStream_t st) {
     X(20, 256, 256, 128, 2, 4)     \
     X(21, 256, 256, 128, 2, 2)     \
     X(22, 256, 128, 128, 2, 4)     \
-    X(23, 128, 128, 128, 2, 2)
+    X(23, 128, 128, 128, 2, 2)     \
+    X(24, 256, 256, 128, 2, 4, true)  \
+    X(25, 256, 128, 128, 2, 4, true)
 
 template <int MODE, bool NORMP>
 bool lg_mode(int cfg, const PPArgs& a, hipStream_t st) {
     switch (cfg) {
-#define LG_CASE(ID, WN_, XM_, RB_, ST_, NWX_) \
-    case ID: lg_launch<WN_, XM_, RB_, ST_, MODE, NORMP, NWX_>(a, st); return true;
+#define LG_CASE(ID, WN_, XM_, RB_, ST_, NWX_, ...) \
+    case ID: lg_launch<WN_, XM_, RB_, ST_, MODE, NORMP, NWX_, 0, ##__VA_ARGS__>(a, st); return true;
         LG_CONFIGS(LG_CASE)
 #undef LG_CASE
         default: break;
@@ -520,6 +578,7 @@ bool lg_mode(int cfg, const PPArgs& a, hipStream_t st) {
             case 58: lg_launch<256, 256, 128, 2, MODE, NORMP, 4, 14>(a, st); return true;
             case 59: lg_launch<256, 256, 128, 2, MODE, NORMP, 4, 12>(a, st); return true;
             case 60: lg_launch<256, 256, 128, 2, MODE, NORMP, 4, 2>(a, st); return true;
+            case 61: lg_launch<256, 256, 128, 2, MODE, NORMP, 4, 4, true>(a, st); return true;
             default: break;
         }
     }
@@ -531,7 +590,7 @@ bool lg_mode(int cfg, const PPArgs& a, hipStream_t st) {
 int gemm_lg_xm(int cfg) {
     if (cfg >= 40) return 256;  // ablation ids
     switch (cfg) {
-#define LG_XM(ID, WN_, XM_, RB_, ST_, NWX_) case ID: return XM_;
+#define LG_XM(ID, WN_, XM_, RB_, ST_, NWX_, ...) case ID: return XM_;
         LG_CONFIGS(LG_XM)
 #undef LG_XM
         default: return 0;
@@ -540,7 +599,7 @@ int gemm_lg_xm(int cfg) {
 int gemm_lg_wn(int cfg) {
     if (cfg >= 40) return 256;
     switch (cfg) {
-#define LG_WN(ID, WN_, XM_, RB_, ST_, NWX_) case ID: return WN_;
+#define LG_WN(ID, WN_, XM_, RB_, ST_, NWX_, ...) case ID: return WN_;
         LG_CONFIGS(LG_WN)
 #undef LG_WN
         default: return 0;

@@ -31,9 +31,6 @@ _FUSE_NORM = os.environ.get("CHRONOS_FUSE_NORM", "1") != "0"
 _FUSE_AR_NORM = os.environ.get("CHRONOS_FUSE_AR_NORM", "1") != "0"  # TP: fused IPC all-reduce + residual + RMSNorm
 # batched decode (>= 2048 (row, kv head) items, bf16 KV): RoPE + paged-KV write fused into the decode attention
 _FUSE_DECODE_ROPE = os.environ.get("CHRONOS_FUSE_DECODE_ROPE", "1") != "0"
-# single stream (T = 1, TP = 1, bf16 KV): attention + O GEMV + residual epilogue in one persistent launch.  Off by
-# default: first measurement 3.04 ms/token against 2.81 for the separate kernels (profiles/r3_attn_o_ab.*)
-_FUSE_ATTN_O = os.environ.get("CHRONOS_FUSE_ATTN_O", "0") == "1"
 
 
 @dataclass
@@ -626,13 +623,6 @@ class LlamaModel:
                 x, lw.wqkv, sb.pos, sb.tok_seq, sb.block_table, self.cos_sin, st["q_buf"], kv.k[li], kv.v[li],
                 self.hq, self.hkv, kv.k_scale[li], kv.v_scale[li])):
             # decode: QKV GEMV (+ folded norm) + RoPE / paged-KV write in one launch
-            if (_FUSE_ATTN_O and T == 1 and sb.nsplit == 1 and self.tp.world == 1 and self.w.norms_folded
-                    and sb.cp is None and kv.k[li].dtype == torch.bfloat16):
-                # single stream: attention + O GEMV + residual epilogue in one persistent launch
-                r = ops.attn_o(st["q_buf"], kv.k[li], kv.v[li], sb.block_table, sb.ctx_len, lw.wo, st["resid"],
-                               self.scale)
-                if r is not None:
-                    return r
             attn = ops.paged_attention(st["q_buf"], kv.k[li], kv.v[li], sb.block_table, sb.q_start, sb.ctx_len,
                                        sb.tiles, sb.ntiles, sb.nqt, sb.nsplit, self.scale, kv.k_scale[li],
                                        kv.v_scale[li]).view(T, -1)

@@ -218,21 +218,6 @@ def paged_attention(q, k_cache, v_cache, block_table, q_start, ctx_len, tiles=No
                                k_scale, v_scale)
 
 
-def attn_o(q, k_cache, v_cache, block_table, ctx_len, w, resid, scale: float, grid_cap: int = 0):
-    """Single-stream decode (one token, TP = 1, bf16 KV, one kv split): attention + O projection + residual epilogue
-    in ONE persistent launch (csrc/kernels/decode_fused.hip) — the O weights stream while the attention runs.
-    Returns the ResidOut that ``gemv_resid(paged_attention(...), w, resid)`` would (bit-identical), or None when the
-    fused kernel does not take the shape."""
-    if not q.is_cuda:
-        return None
-    if _checking(q):
-        _check_paged(block_table[:1], k_cache, torch.arange(1), ctx_len[:1], "attn_o")
-    s, part = _k().attn_o(q, k_cache, v_cache, block_table, ctx_len, w, resid, scale, grid_cap)
-    if s is None or s.numel() == 0:  # declined (an undefined tensor comes back as None)
-        return None
-    return ResidOut(s, part)
-
-
 def decode_attention_rope(qkv, pos, cos_sin, k_cache, v_cache, block_table, ctx_len, n: int, hq: int,
                           scale: float):
     """Decode step (row i = sequence i, one token at pos[i], ctx_len[i] == pos[i] + 1): RoPE + paged-KV write + paged
