@@ -51,7 +51,7 @@ def candidates(m, n, k, mode, keep=6):
     from chronos.ops import gemm as G
 
     scored = []
-    for cfg in G._PP_BM:
+    for cfg in [c for c in G._PP_BM if c < G.LG_FIRST]:
         bm, bn = G._PP_BM[cfg], G._PP_BN[cfg]
         tiles = -(-m // bm) * -(-n // bn)
         for sk in (1, 2, 4, 8):
@@ -67,6 +67,16 @@ def candidates(m, n, k, mode, keep=6):
     for must in ((0, 1), (4, 1), (8, 1)):
         if must not in out and G._pp_valid(must[0], n, k, mode, 1):
             out.append(must)
+    # the software-pipelined family (gemm_lg.hip): every slab / ring config that tiles the shape, split-K where the
+    # tile grid under-fills the chip
+    if m >= 256:
+        for cfg in (24, 25, 20, 22, 23, 19):
+            bm, bn = G._PP_BM[cfg], G._PP_BN[cfg]
+            tiles = -(-m // bm) * -(-n // bn)
+            for sk in (1, 2, 4):
+                if G._pp_valid(cfg, n, k, mode, sk) and (sk == 1 or (tiles < 256 and tiles * sk <= 768)) \
+                        and (cfg, sk) not in out:
+                    out.append((cfg, sk))
     # split-K of the widest tiles where the tile grid under-fills the chip (the fence-free split costs ~2-5 us)
     for cfg in (0, 4, 3):
         bm, bn = G._PP_BM[cfg], G._PP_BN[cfg]

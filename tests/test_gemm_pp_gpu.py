@@ -62,7 +62,7 @@ def test_n_tail(cfg):
 
 
 @pytest.mark.parametrize("cfg,splitk", [(0, 2), (1, 4), (3, 2), (2, 5), (4, 2), (5, 4), (7, 2), (8, 2), (9, 4), (10, 2), (11, 5),
-                                        (12, 2), (13, 4), (14, 5), (15, 2), (16, 2), (17, 4), (18, 5), (19, 2), (20, 2), (21, 4), (22, 5), (23, 2), (24, 2), (25, 3)])
+                                        (12, 2), (13, 4), (14, 5), (15, 2), (16, 2), (17, 4), (18, 5), (19, 2), (20, 2), (21, 4), (22, 5), (23, 2), (24, 2), (25, 4)])
 def test_splitk(cfg, splitk):
     g = torch.Generator(device=DEV).manual_seed(11 + cfg)
     m, n, k = 300, 512, 64 * 20
