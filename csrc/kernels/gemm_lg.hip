@@ -86,6 +86,16 @@ __device__ __forceinline__ void lg_dma16(const void* base, int bytes, unsigned c
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)dst, 16, voff, soff, 0, 0);
 }
 
+// The same piece as inline asm (VAR 2): M0 = the LDS destination, written in the same statement that reads it
+// (cdna_hip_programming.md §5.7).  No VGPR destination; completion is counted by the kernel's own vmcnt waits.
+typedef int lg_i32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void lg_dma16_asm(const void* base, int bytes, uint32_t lds, uint32_t voff, int soff) {
+    const uint64_t b = (uint64_t)base;
+    const lg_i32x4 r = {(int)(uint32_t)b, (int)(uint32_t)(b >> 32), bytes, 0x00020000};
+    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds"
+                 ::"v"(voff), "s"(r), "s"(lds), "s"(soff) : "memory");
+}
+
 // 64-B-row chunk swizzle (the 16x16x32 fragment reads of a 16-row block land on 16 distinct 16-B slots)
 __device__ __forceinline__ int lg_swz64(int row) { return (4 - ((row >> 2) & 3)) & 3; }
 
@@ -93,8 +103,13 @@ __device__ __forceinline__ int lg_swz64(int row) { return (4 - ((row >> 2) & 3))
 // 8 every tile's DMA sources aliased onto tile (0, 0) (operands L2-resident)
 // STG (slab schedule, 8 waves): the slab's DMA is split between the wave groups — waves 0-3 issue theirs in k-step B,
 // waves 4-7 (their SIMD partners) in the next k-step A — so one wave of each SIMD issues DMA while the other runs MFMAs
-template <int WN, int XM, int RB, int ST, int MODE, bool NORMP, int NWX, int ABL = 0, bool STG = false>
+// VAR (slab schedule): 0 the compiler places the DMA by sched_group_barrier (every DMA before the block's first
+// ds_read), 1 STG, 2 MAN: each k-step written out in issue order, DMA pieces as inline-asm buffer_load ... lds spread
+// evenly through k-step B among the MFMAs and ds_reads (hipcc cannot see an asm DMA write LDS, so it adds no
+// lgkmcnt wait in front of it; the ring buffers it writes are disjoint from the ones being read by construction)
+template <int WN, int XM, int RB, int ST, int MODE, bool NORMP, int NWX, int ABL = 0, int VAR = 0>
 __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
+    constexpr bool STG = VAR == 1, MAN = VAR == 2;
     constexpr int NW = 2 * NWX;                       // waves: 2 along W x NWX along x (NWX = 4: two per SIMD)
     constexpr int RPI = 1024 / RB;                    // image rows per LDS-DMA instruction
     constexpr int KS = RB / 64;                       // 32-deep k-steps per stage
@@ -111,6 +126,7 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
     // slab); ST >= 3: the ring schedule (DMA of stage t+ST-1 into the buffer of stage t-1)
     constexpr bool SLAB = ST == 2;
     static_assert(!STG || (SLAB && NWX == 4), "staggered DMA: slab schedule, two waves per SIMD");
+    static_assert(!MAN || SLAB, "issue-ordered k-steps: slab schedule");
     static_assert(ST >= 3 || (SLAB && RB == 128), "slab schedule: 64-deep (128-B row) slabs");
     static_assert(MODE != kSwiglu || (WN / 4) % 16 == 0, "swiglu: WN/4 gate rows per wave, multiple of 16");
     static_assert(RB == 64 || RB == 128, "stage depth 32 or 64");
@@ -283,6 +299,50 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
         rd(0, 0, fa0, fb0);
         // STG: one straight-line loop per wave group (the DMA sits in a different k-step), so each keeps its
         // compile-time interleave
+        // MAN: k-step in issue order.  MFMA i of the block is (W block i / MT, x block i % MT); DMA piece d goes before
+        // MFMA d * DS, fragment read r after MFMA r * RS + RS - 1 (the last quarter of the block reads nothing)
+        auto kstep_man = [&](auto DMA_ON, bf16x8 (&fa)[NT], bf16x8 (&fb)[MT], int jr, int kkr, bf16x8 (&na)[NT],
+                             bf16x8 (&nb)[MT], int jd) {
+            constexpr bool dma_on = decltype(DMA_ON)::value;
+            constexpr int DS = MF / NPER > 0 ? MF / NPER : 1;
+            constexpr int RS = (MF - MF / 4) / NR > 0 ? (MF - MF / 4) / NR : 1;
+            const unsigned char* wb = smem + (jr & 1) * STAGE;
+            const unsigned char* xb = wb + WIMG;
+            unsigned char* db = smem + (jd & 1) * STAGE;
+            const int kb = min(jd, NS1) * RB;
+#pragma unroll
+            for (int i = 0; i < MF; ++i) {
+                if constexpr (dma_on) {
+                    if (i % DS == 0 && i / DS < NPER) {
+                        const int d = i / DS;
+                        lg_dma16_asm(isw[d] ? (const void*)a.w : (const void*)a.x, isw[d] ? wbytes : xbytes,
+                                     (uint32_t)__builtin_amdgcn_readfirstlane((int)(uintptr_t)(db + dsto[d])),
+                                     voff[d], kb);
+                    }
+                }
+                if constexpr (!(ABL & 4))
+                    acc[i / MT][i % MT] =
+                        __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i / MT], fb[i % MT], acc[i / MT][i % MT], 0, 0, 0);
+                else
+                    asm volatile("" ::"v"(fa[i / MT]), "v"(fb[i % MT]));
+                if (!(ABL & 2) && i % RS == RS - 1 && i / RS < NR) {
+                    const int r = i / RS;
+                    if (r < NT) na[r] = *reinterpret_cast<const bf16x8*>(wb + wrow0[r] * RB + loff[kkr]);
+                    else nb[r - NT] = *reinterpret_cast<const bf16x8*>(xb + (xrow0 + 16 * (r - NT)) * RB + loff[kkr]);
+                }
+                // pin the order at every DMA slot (hipcc would otherwise sink the asm pieces to the block's end)
+                if (i % DS == DS - 1) __builtin_amdgcn_sched_barrier(0);
+            }
+        };
+        if constexpr (MAN) {
+            for (int j = 0; j < NS; ++j) {
+                kstep_man(std::integral_constant<bool, false>{}, fa0, fb0, j, 1, fa1, fb1, 0);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                lg_vmcnt<0>();
+                lg_bar();
+                kstep_man(std::integral_constant<bool, true>{}, fa1, fb1, j + 1, 0, fa0, fb0, j + 2);
+            }
+        }
         auto loop_stg = [&](auto G) {
             constexpr int g = decltype(G)::value;
             for (int j = 0; j < NS; ++j) {
@@ -303,7 +363,8 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
                 __builtin_amdgcn_sched_barrier(0);
             }
         };
-        if constexpr (STG) {
+        if constexpr (MAN) {
+        } else if constexpr (STG) {
             if (grp == 0) loop_stg(std::integral_constant<int, 0>{});
             else loop_stg(std::integral_constant<int, 1>{});
         } else
@@ -518,10 +579,10 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
     }
 }
 
-template <int WN, int XM, int RB, int ST, int MODE, bool NORMP, int NWX, int ABL = 0, bool STG = false>
+template <int WN, int XM, int RB, int ST, int MODE, bool NORMP, int NWX, int ABL = 0, int VAR = 0>
 void lg_launch(const PPArgs& a, hipStream_t st) {
     const int lds = ST * (WN + XM) * RB + 16 + XM * 4;
-    auto kern = gemm_lg_kernel<WN, XM, RB, ST, MODE, NORMP, NWX, ABL, STG>;
+    auto kern = gemm_lg_kernel<WN, XM, RB, ST, MODE, NORMP, NWX, ABL, VAR>;
     static bool attr = false;
     if (!attr) {
         hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
@@ -547,8 +608,11 @@ void lg_launch(const PPArgs& a, hipStream_t st) {
     X(21, 256, 256, 128, 2, 2)     \
     X(22, 256, 128, 128, 2, 4)     \
     X(23, 128, 128, 128, 2, 2)     \
-    X(24, 256, 256, 128, 2, 4, true)  \
-    X(25, 256, 128, 128, 2, 4, true)
+    X(24, 256, 256, 128, 2, 4, 1)  \
+    X(25, 256, 128, 128, 2, 4, 1)  \
+    X(26, 256, 256, 128, 2, 4, 2)  \
+    X(27, 256, 128, 128, 2, 4, 2)  \
+    X(28, 128, 128, 128, 2, 2, 2)
 
 template <int MODE, bool NORMP>
 bool lg_mode(int cfg, const PPArgs& a, hipStream_t st) {
@@ -578,7 +642,9 @@ bool lg_mode(int cfg, const PPArgs& a, hipStream_t st) {
             case 58: lg_launch<256, 256, 128, 2, MODE, NORMP, 4, 14>(a, st); return true;
             case 59: lg_launch<256, 256, 128, 2, MODE, NORMP, 4, 12>(a, st); return true;
             case 60: lg_launch<256, 256, 128, 2, MODE, NORMP, 4, 2>(a, st); return true;
-            case 61: lg_launch<256, 256, 128, 2, MODE, NORMP, 4, 4, true>(a, st); return true;
+            case 61: lg_launch<256, 256, 128, 2, MODE, NORMP, 4, 4, 1>(a, st); return true;
+            case 62: lg_launch<256, 256, 128, 2, MODE, NORMP, 4, 4, 2>(a, st); return true;
+            case 63: lg_launch<256, 256, 128, 2, MODE, NORMP, 4, 2, 2>(a, st); return true;
             default: break;
         }
     }
