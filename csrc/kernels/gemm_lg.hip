@@ -612,7 +612,10 @@ void lg_launch(const PPArgs& a, hipStream_t st) {
     X(25, 256, 128, 128, 2, 4, 1)  \
     X(26, 256, 256, 128, 2, 4, 2)  \
     X(27, 256, 128, 128, 2, 4, 2)  \
-    X(28, 128, 128, 128, 2, 2, 2)
+    X(28, 128, 128, 128, 2, 2, 2)  \
+    X(29, 256, 128, 128, 3, 4)     \
+    X(30, 128, 256, 128, 3, 4)     \
+    X(31, 128, 128, 128, 3, 2)
 
 template <int MODE, bool NORMP>
 bool lg_mode(int cfg, const PPArgs& a, hipStream_t st) {

@@ -70,7 +70,7 @@ def candidates(m, n, k, mode, keep=6):
     # the software-pipelined family (gemm_lg.hip): every slab / ring config that tiles the shape, split-K where the
     # tile grid under-fills the chip
     if m >= 256:
-        for cfg in (24, 25, 20, 22, 23, 19):
+        for cfg in (20, 29, 30, 19, 31, 23):
             bm, bn = G._PP_BM[cfg], G._PP_BN[cfg]
             tiles = -(-m // bm) * -(-n // bn)
             for sk in (1, 2, 4):
@@ -201,7 +201,13 @@ def main():
         for key, rows in merged.items():  # shapes not measured in this run
             plans.setdefault(key, rows)
         with open(args.out_plan, "w") as fh:
-            json.dump({"meta": meta, "plans": plans}, fh, indent=1)
+            out = {"meta": meta, "plans": plans}
+            if args.merge:  # the fp8 routing rows (--fp8 runs) travel with the plan file
+                with open(args.merge) as mf:
+                    q = json.load(mf).get("qplans")
+                if q:
+                    out["qplans"] = q
+            json.dump(out, fh, indent=1)
     if args.out_table:
         with open(args.out_table, "w") as fh:
             fh.writelines(json.dumps(r) + "\n" for r in table)

@@ -35,7 +35,7 @@ def _check(y, ref, tol=2e-2):
     assert err <= tol * scale, f"max err {err:.4g} vs max |ref| {scale:.4g}"
 
 
-LG = [12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28]  # gemm_lg.hip configs (12-19 ring schedule, 20-23 slab schedule)
+LG = [12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31]  # gemm_lg.hip configs (12-19 ring schedule, 20-23 slab schedule)
 CFGS = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11] + LG
 
 
@@ -62,7 +62,7 @@ def test_n_tail(cfg):
 
 
 @pytest.mark.parametrize("cfg,splitk", [(0, 2), (1, 4), (3, 2), (2, 5), (4, 2), (5, 4), (7, 2), (8, 2), (9, 4), (10, 2), (11, 5),
-                                        (12, 2), (13, 4), (14, 5), (15, 2), (16, 2), (17, 4), (18, 5), (19, 2), (20, 2), (21, 4), (22, 5), (23, 2), (24, 2), (25, 4), (26, 2), (27, 4), (28, 5)])
+                                        (12, 2), (13, 4), (14, 5), (15, 2), (16, 2), (17, 4), (18, 5), (19, 2), (20, 2), (21, 4), (22, 5), (23, 2), (24, 2), (25, 4), (26, 2), (27, 4), (28, 5), (29, 2), (30, 4), (31, 5)])
 def test_splitk(cfg, splitk):
     g = torch.Generator(device=DEV).manual_seed(11 + cfg)
     m, n, k = 300, 512, 64 * 20
@@ -94,7 +94,7 @@ def test_swiglu_normp(cfg):
 
 
 @pytest.mark.parametrize("cfg,splitk", [(0, 1), (1, 2), (3, 1), (4, 1), (5, 2), (8, 1), (9, 2), (10, 1),
-                                        (12, 1), (12, 2), (13, 1), (14, 2), (15, 1), (16, 1), (17, 2), (18, 1), (19, 2), (20, 1), (20, 2), (21, 1), (22, 2), (23, 1), (24, 1), (24, 2), (25, 1), (26, 1), (26, 2), (27, 1), (28, 2)])
+                                        (12, 1), (12, 2), (13, 1), (14, 2), (15, 1), (16, 1), (17, 2), (18, 1), (19, 2), (20, 1), (20, 2), (21, 1), (22, 2), (23, 1), (24, 1), (24, 2), (25, 1), (26, 1), (26, 2), (27, 1), (28, 2), (29, 1), (30, 2), (31, 1)])
 def test_resid_partials(cfg, splitk):
     g = torch.Generator(device=DEV).manual_seed(5 + cfg)
     m, n, k = 259, 512, 768
