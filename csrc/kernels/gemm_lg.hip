@@ -100,7 +100,8 @@ __device__ __forceinline__ void lg_dma16_asm(const void* base, int bytes, uint32
 __device__ __forceinline__ int lg_swz64(int row) { return (4 - ((row >> 2) & 3)) & 3; }
 
 // ABL (timing diagnostics only, plain mode): 1 no DMA in the loop, 2 no fragment reads in the loop, 4 no MFMA,
-// 8 every tile's DMA sources aliased onto tile (0, 0) (operands L2-resident)
+// 8 every tile's DMA sources aliased onto tile (0, 0) (operands L2-resident), 16 (slab) no vmcnt wait before the
+// barrier, 32 (slab) no barrier either — 16/32 read LDS the DMA may not have filled: timing only, wrong results
 // STG (slab schedule, 8 waves): the slab's DMA is split between the wave groups — waves 0-3 issue theirs in k-step B,
 // waves 4-7 (their SIMD partners) in the next k-step A — so one wave of each SIMD issues DMA while the other runs MFMAs
 // VAR (slab schedule): 0 the compiler places the DMA by sched_group_barrier (every DMA before the block's first
@@ -381,8 +382,8 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
             lg_sched<0, MF, 0, NR>();
             __builtin_amdgcn_sched_barrier(0);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            lg_vmcnt<0>();
-            lg_bar();
+            if constexpr (!(ABL & 16)) lg_vmcnt<0>();  // (ABL 16/32: timing only, races by design)
+            if constexpr (!(ABL & 32)) lg_bar();
             // k-step B
             if constexpr (!(ABL & 1)) issue(j + 2);
             if constexpr (!(ABL & 2)) rd(j + 1, 0, fa0, fb0);
@@ -648,6 +649,9 @@ bool lg_mode(int cfg, const PPArgs& a, hipStream_t st) {
             case 61: lg_launch<256, 256, 128, 2, MODE, NORMP, 4, 4, 1>(a, st); return true;
             case 62: lg_launch<256, 256, 128, 2, MODE, NORMP, 4, 4, 2>(a, st); return true;
             case 63: lg_launch<256, 256, 128, 2, MODE, NORMP, 4, 2, 2>(a, st); return true;
+            case 64: lg_launch<256, 256, 128, 2, MODE, NORMP, 4, 16>(a, st); return true;
+            case 65: lg_launch<256, 256, 128, 2, MODE, NORMP, 4, 48>(a, st); return true;
+            case 66: lg_launch<256, 256, 128, 2, MODE, NORMP, 4, 48 | 2>(a, st); return true;
             default: break;
         }
     }

@@ -23,13 +23,18 @@ __device__ __forceinline__ void vmcnt() {
     __builtin_amdgcn_s_waitcnt((N & 0xF) | (0x7 << 4) | (0xF << 8) | ((N >> 4) << 14));
 }
 
-template <int I, int MF, int NV>
+// MFMA i is preceded by its share of the NV loads and followed by its share of the NR ds_reads; HEAD: every load
+// before the first MFMA, the reads spread over the MFMAs after the first NV
+template <int I, int MF, int NV, int NR, bool HEAD>
 __device__ __forceinline__ void sched() {
     if constexpr (I < MF) {
-        constexpr int v = (I + 1) * NV / MF - I * NV / MF;
+        constexpr int v = HEAD ? (I == 0 ? NV : 0) : (I + 1) * NV / MF - I * NV / MF;
+        constexpr int R0 = HEAD ? (NV < MF ? NV : 0) : 0;
+        constexpr int r = I < R0 ? 0 : (I - R0 + 1) * NR / (MF - R0) - (I - R0) * NR / (MF - R0);
         if constexpr (v > 0) __builtin_amdgcn_sched_group_barrier(0x010, v, 0);
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        sched<I + 1, MF, NV>();
+        if constexpr (r > 0) __builtin_amdgcn_sched_group_barrier(0x100, r, 0);
+        sched<I + 1, MF, NV, NR, HEAD>();
     }
 }
 
@@ -39,12 +44,14 @@ __device__ __forceinline__ void dma_buf(const void* base, unsigned char* dst, ui
     __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_ptr_t)dst, 16, voff, 0, 0, 0);
 }
 
-template <int NMF, int NDMA, int KIND>
+template <int NMF, int NDMA, int KIND, int NRD = 0, bool HEAD = false>
 __global__ void __launch_bounds__(512, 1) kern(const uint16_t* src, float* out, long long* cyc, int iters) {
     extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const bf16x8 a = *reinterpret_cast<const bf16x8*>(src + lane * 8);
-    const bf16x8 b = *reinterpret_cast<const bf16x8*>(src + 512 + lane * 8);
+    bf16x8 a = *reinterpret_cast<const bf16x8*>(src + lane * 8);
+    bf16x8 b = *reinterpret_cast<const bf16x8*>(src + 512 + lane * 8);
+    bf16x8 rf[NRD > 0 ? NRD : 1];
+    const unsigned char* rsrc = smem + 65536 - 16384 + (lane & 15) * 128 + (((lane >> 4) ^ (lane & 7)) << 4);
     f32x4 acc[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -66,7 +73,13 @@ __global__ void __launch_bounds__(512, 1) kern(const uint16_t* src, float* out, 
         }
 #pragma unroll
         for (int i = 0; i < NMF; ++i) acc[i & 7] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[i & 7], 0, 0, 0);
-        sched<0, NMF, NDMA>();
+#pragma unroll
+        for (int r = 0; r < NRD; ++r) rf[r] = *reinterpret_cast<const bf16x8*>(rsrc + (r & 7) * 2048);
+        sched<0, NMF, NDMA, NRD, HEAD>();
+        if constexpr (NRD > 0) {
+#pragma unroll
+            for (int r = 0; r < NRD; ++r) asm volatile("" ::"v"(rf[r]));
+        }
         __builtin_amdgcn_sched_barrier(0);
         if constexpr (KIND == 2 && NDMA > 0) {
 #pragma unroll
@@ -84,10 +97,10 @@ __global__ void __launch_bounds__(512, 1) kern(const uint16_t* src, float* out, 
     if (lane == 0) cyc[blockIdx.x * 8 + wave] = t1 - t0;
 }
 
-template <int NMF, int NDMA, int KIND>
+template <int NMF, int NDMA, int KIND, int NRD = 0, bool HEAD = false>
 void run(const char* name, int waves, const uint16_t* src, float* out, long long* cyc) {
     const int iters = 2000, grid = 256;
-    auto k = kern<NMF, NDMA, KIND>;
+    auto k = kern<NMF, NDMA, KIND, NRD, HEAD>;
     hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
     for (int rep = 0; rep < 2; ++rep) hipLaunchKernelGGL(k, dim3(grid), dim3(64 * waves), 65536, 0, src, out, cyc, iters);
     hipDeviceSynchronize();
@@ -95,12 +108,17 @@ void run(const char* name, int waves, const uint16_t* src, float* out, long long
     hipMemcpy(h.data(), cyc, h.size() * 8, hipMemcpyDeviceToHost);
     double sum = 0;
     int n = 0;
-    for (int b = 0; b < grid; ++b)
-        for (int w = 0; w < waves; ++w) sum += h[b * 8 + w], ++n;
+    // the slowest wave of each workgroup (two waves on a SIMD share it: the younger one finishes last)
+    for (int b = 0; b < grid; ++b) {
+        long long mx = 0;
+        for (int w = 0; w < waves; ++w) mx = h[b * 8 + w] > mx ? h[b * 8 + w] : mx;
+        sum += mx, ++n;
+    }
     const double per = sum / n / iters;
     const double util = (waves / 4.0) * NMF * 16 / per;
-    printf("{\"case\": \"%s\", \"waves_per_simd\": %d, \"mfma\": %d, \"dma\": %d, \"kind\": %d, \"cyc_per_iter\": %.1f, "
-           "\"mfma_pipe_util\": %.3f}\n", name, waves / 4, NMF, NDMA, KIND, per, util);
+    printf("{\"case\": \"%s\", \"waves_per_simd\": %d, \"mfma\": %d, \"dma\": %d, \"kind\": %d, \"reads\": %d, "
+           "\"dma_head\": %d, \"cyc_per_iter\": %.1f, \"mfma_pipe_util\": %.3f}\n", name, waves / 4, NMF, NDMA, KIND,
+           NRD, (int)HEAD, per, util);
 }
 
 int main() {
@@ -113,12 +131,14 @@ int main() {
     hipMalloc(&cyc, 256 * 8 * 8);
     for (int waves : {4, 8}) {
         run<32, 0, 0>("mfma only", waves, src, out, cyc);
-        run<32, 2, 0>("buffer lds x2", waves, src, out, cyc);
-        run<32, 4, 0>("buffer lds x4", waves, src, out, cyc);
         run<32, 8, 0>("buffer lds x8", waves, src, out, cyc);
-        run<32, 8, 1>("global lds x8", waves, src, out, cyc);
-        run<32, 8, 2>("global vgpr x8", waves, src, out, cyc);
-        run<64, 8, 0>("buffer lds x8 / 64 mfma", waves, src, out, cyc);
+        run<32, 0, 0, 12>("reads x12", waves, src, out, cyc);
+        run<32, 8, 0, 12>("buffer lds x8 + reads x12 interleaved", waves, src, out, cyc);
+        run<32, 8, 0, 12, true>("buffer lds x8 head + reads x12", waves, src, out, cyc);
+        run<32, 4, 0, 12>("buffer lds x4 + reads x12", waves, src, out, cyc);
+        run<64, 16, 0, 16>("128x128/wave: 64 mfma, 16 dma, 16 reads", waves, src, out, cyc);
+        run<64, 16, 0, 16, true>("128x128/wave: 64 mfma, 16 dma head, 16 reads", waves, src, out, cyc);
+        run<32, 8, 2, 12>("global vgpr x8 + reads x12", waves, src, out, cyc);
     }
     hipFree(src);
     hipFree(out);
