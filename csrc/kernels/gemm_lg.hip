@@ -595,7 +595,9 @@ void lg_launch(const PPArgs& a, hipStream_t st) {
 }
 
 // tile configs (ids continue gemm_pp's): {WN = W rows, XM = x rows, RB = LDS row bytes (BK = RB/2), ST = ring depth,
-// NWX = waves along x (2: one wave per SIMD; 4: two)}
+// NWX = waves along x (2: one wave per SIMD; 4: two)}.  32-39: mid-M (64-256 rows) weight streaming — 64 W rows per
+// workgroup so the tile grid x split-K covers the chip with few slices, the whole x panel shared by the W-row waves
+// through LDS (x bytes <= 2-4x the weight bytes per workgroup, L2-resident), a 4-6 stage ring for the HBM latency
 #define LG_CONFIGS(X)              \
     X(12, 256, 256, 64, 4, 2)      \
     X(13, 256, 128, 64, 6, 2)      \
@@ -616,7 +618,15 @@ void lg_launch(const PPArgs& a, hipStream_t st) {
     X(28, 128, 128, 128, 2, 2, 2)  \
     X(29, 256, 128, 128, 3, 4)     \
     X(30, 128, 256, 128, 3, 4)     \
-    X(31, 128, 128, 128, 3, 2)
+    X(31, 128, 128, 128, 3, 2)     \
+    X(32, 64, 128, 128, 4, 2)      \
+    X(33, 64, 64, 128, 4, 2)       \
+    X(34, 64, 128, 128, 6, 2)      \
+    X(35, 64, 256, 128, 3, 4)      \
+    X(36, 64, 64, 128, 8, 2)       \
+    X(37, 64, 128, 128, 5, 2)      \
+    X(38, 128, 64, 128, 6, 2)      \
+    X(39, 64, 64, 128, 6, 2)
 
 template <int MODE, bool NORMP>
 bool lg_mode(int cfg, const PPArgs& a, hipStream_t st) {

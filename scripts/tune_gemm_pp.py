@@ -77,6 +77,18 @@ def candidates(m, n, k, mode, keep=6):
                 if G._pp_valid(cfg, n, k, mode, sk) and (sk == 1 or (tiles < 256 and tiles * sk <= 768)) \
                         and (cfg, sk) not in out:
                     out.append((cfg, sk))
+    # mid-M weight streaming (gemm_lg.hip 32-39: 64 W rows, the x panel shared through LDS, 4-8 stage rings), split-K
+    # until the grid covers the chip
+    if 48 <= m <= 512:
+        for cfg in (32, 33, 34, 35, 36, 37, 38, 39, 15):
+            bm, bn = G._PP_BM[cfg], G._PP_BN[cfg]
+            tiles = -(-m // bm) * -(-n // bn)
+            if bm > 2 * m and cfg != 33 and cfg != 36 and cfg != 39:
+                continue  # x tile far taller than M
+            for sk in (1, 2, 4, 8):
+                if G._pp_valid(cfg, n, k, mode, sk) and (sk == 1 or (tiles < 256 and tiles * sk <= 1024)) \
+                        and (cfg, sk) not in out:
+                    out.append((cfg, sk))
     # split-K of the widest tiles where the tile grid under-fills the chip (the fence-free split costs ~2-5 us)
     for cfg in (0, 4, 3):
         bm, bn = G._PP_BM[cfg], G._PP_BN[cfg]
