@@ -30,6 +30,7 @@ bool launch_gemm_pp(int cfg, int mode, bool normp, bool prio, const PPArgs& a, h
 // large-M family (csrc/kernels/gemm_lg.hip): config ids kPPConfigs .. kPPConfigs + kLGConfigs - 1 of the same PPArgs
 // interface; tile = WN W rows x XM x rows, 4 or 8 waves (2 x NWX), kResid partials are [M, N / (WN / 2)]
 constexpr int kLGConfigs = 28;
+constexpr int kLGTinyFirst = 72, kLGTinyConfigs = 4;  // gemm_lg 72-75 (after the 40-71 timing-ablation ids)
 int gemm_lg_xm(int cfg);  // x rows per tile
 int gemm_lg_wn(int cfg);  // W rows per tile
 bool launch_gemm_lg(int cfg, int mode, bool normp, const PPArgs& a, hipStream_t st);

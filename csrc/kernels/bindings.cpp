@@ -500,7 +500,8 @@ std::tuple<Tensor, Tensor> gemm_pp(const Tensor& x, const Tensor& w, int64_t mod
     const int64_t K = x.size(-1), M = x.numel() / K, N = w.size(0);
     CHK(w.dim() == 2 && w.size(1) == K, "gemm_pp: w must be [N, K]");
     const bool lg = cfg >= chronos::kPPConfigs;  // gemm_lg.hip configs continue the id space
-    CHK((cfg >= 0 && cfg < chronos::kPPConfigs + chronos::kLGConfigs) || (cfg >= 40 && cfg < 72), "gemm_pp: cfg");
+    CHK((cfg >= 0 && cfg < chronos::kPPConfigs + chronos::kLGConfigs) || (cfg >= 40 && cfg < 72) ||
+            (cfg >= chronos::kLGTinyFirst && cfg < chronos::kLGTinyFirst + chronos::kLGTinyConfigs), "gemm_pp: cfg");
     CHK(mode >= 0 && mode <= 2, "gemm_pp: mode");
     const int BM = lg ? chronos::gemm_lg_xm((int)cfg) : chronos::gemm_pp_bm((int)cfg);
     const int BN = lg ? chronos::gemm_lg_wn((int)cfg) : chronos::gemm_pp_bn((int)cfg);

@@ -595,7 +595,8 @@ void lg_launch(const PPArgs& a, hipStream_t st) {
 }
 
 // tile configs (ids continue gemm_pp's): {WN = W rows, XM = x rows, RB = LDS row bytes (BK = RB/2), ST = ring depth,
-// NWX = waves along x (2: one wave per SIMD; 4: two)}.  32-39: mid-M (64-256 rows) weight streaming — 64 W rows per
+// NWX = waves along x (2: one wave per SIMD; 4: two)}.  72-75 (ids after the ablation range): 32 x rows for
+// M <= 32 (jump-forward forwards, drained buckets).  32-39: mid-M (64-256 rows) weight streaming — 64 W rows per
 // workgroup so the tile grid x split-K covers the chip with few slices, the whole x panel shared by the W-row waves
 // through LDS (x bytes <= 2-4x the weight bytes per workgroup, L2-resident), a 4-6 stage ring for the HBM latency
 #define LG_CONFIGS(X)              \
@@ -626,7 +627,11 @@ void lg_launch(const PPArgs& a, hipStream_t st) {
     X(36, 64, 64, 128, 8, 2)       \
     X(37, 64, 128, 128, 5, 2)      \
     X(38, 128, 64, 128, 6, 2)      \
-    X(39, 64, 64, 128, 6, 2)
+    X(39, 64, 64, 128, 6, 2)       \
+    X(72, 64, 32, 128, 8, 2)       \
+    X(73, 128, 32, 128, 6, 2)      \
+    X(74, 64, 32, 128, 4, 2)       \
+    X(75, 128, 32, 128, 4, 2)
 
 template <int MODE, bool NORMP>
 bool lg_mode(int cfg, const PPArgs& a, hipStream_t st) {
@@ -671,7 +676,7 @@ bool lg_mode(int cfg, const PPArgs& a, hipStream_t st) {
 }  // namespace
 
 int gemm_lg_xm(int cfg) {
-    if (cfg >= 40) return 256;  // ablation ids
+    if (cfg >= 40 && cfg < 72) return 256;  // ablation ids
     switch (cfg) {
 #define LG_XM(ID, WN_, XM_, RB_, ST_, NWX_, ...) case ID: return XM_;
         LG_CONFIGS(LG_XM)
@@ -680,7 +685,7 @@ int gemm_lg_xm(int cfg) {
     }
 }
 int gemm_lg_wn(int cfg) {
-    if (cfg >= 40) return 256;
+    if (cfg >= 40 && cfg < 72) return 256;
     switch (cfg) {
 #define LG_WN(ID, WN_, XM_, RB_, ST_, NWX_, ...) case ID: return WN_;
         LG_CONFIGS(LG_WN)

@@ -26,12 +26,14 @@ SHAPES = {  # name: (N, K, mode)  mode 1 = swiglu (N = 2F)
 BM = {0: 256, 1: 128, 2: 256, 3: 128, 4: 256, 5: 128, 6: 256, 7: 128, 8: 256, 9: 128, 10: 256, 11: 128,
       12: 256, 13: 128, 14: 256, 15: 128, 16: 256, 17: 128, 18: 256, 19: 128,
       20: 256, 21: 256, 22: 128, 23: 128, 24: 256, 25: 128, 26: 256, 27: 128, 28: 128, 29: 128, 30: 256, 31: 128,
-      32: 128, 33: 64, 34: 128, 35: 256, 36: 64, 37: 128, 38: 64, 39: 64}  # x rows per tile (12+: gemm_lg.hip)
+      32: 128, 33: 64, 34: 128, 35: 256, 36: 64, 37: 128, 38: 64, 39: 64,
+      72: 32, 73: 32, 74: 32, 75: 32}  # x rows per tile (12+: gemm_lg.hip)
 BM.update({c: 256 for c in range(40, 72)})  # gemm_lg timing ablations (40 + 8 * (cfg == 16) + ABL)
 BN = {0: 256, 1: 256, 2: 128, 3: 128, 4: 256, 5: 256, 6: 128, 7: 128, 8: 256, 9: 256, 10: 128, 11: 128,
       12: 256, 13: 256, 14: 128, 15: 128, 16: 256, 17: 256, 18: 128, 19: 128,
       20: 256, 21: 256, 22: 256, 23: 128, 24: 256, 25: 256, 26: 256, 27: 256, 28: 128, 29: 256, 30: 128, 31: 128,
-      32: 64, 33: 64, 34: 64, 35: 64, 36: 64, 37: 64, 38: 128, 39: 64}  # W rows per tile
+      32: 64, 33: 64, 34: 64, 35: 64, 36: 64, 37: 64, 38: 128, 39: 64,
+      72: 64, 73: 128, 74: 64, 75: 128}  # W rows per tile
 BN.update({c: 256 for c in range(40, 72)})
 
 

@@ -47,6 +47,19 @@ def skinny_candidates(m, n, k, mode, keep=10):
     return [(c, sk) for _, _, c, sk in out[:keep]]
 
 
+def tiny_candidates(m, n, k, mode):
+    """M < 16: the 32-row-x-tile gemm_lg configs (72-75), split-K while the tile grid under-fills the chip."""
+    from chronos.ops import gemm as G
+
+    out = []
+    for cfg in (72, 73, 74, 75):
+        tiles = -(-n // G._PP_BN[cfg])
+        for sk in (1, 2, 4, 8):
+            if G._pp_valid(cfg, n, k, mode, sk) and (sk == 1 or (tiles < 256 and tiles * sk <= 1024)):
+                out.append((cfg, sk))
+    return out
+
+
 def candidates(m, n, k, mode, keep=6):
     from chronos.ops import gemm as G
 
@@ -85,6 +98,15 @@ def candidates(m, n, k, mode, keep=6):
             tiles = -(-m // bm) * -(-n // bn)
             if bm > 2 * m and cfg != 33 and cfg != 36 and cfg != 39:
                 continue  # x tile far taller than M
+            for sk in (1, 2, 4, 8):
+                if G._pp_valid(cfg, n, k, mode, sk) and (sk == 1 or (tiles < 256 and tiles * sk <= 1024)) \
+                        and (cfg, sk) not in out:
+                    out.append((cfg, sk))
+    # M <= 48: the same with 32-row x tiles (72-75)
+    if 2 <= m <= 48:
+        for cfg in (72, 73, 74, 75):
+            bm, bn = G._PP_BM[cfg], G._PP_BN[cfg]
+            tiles = -(-m // bm) * -(-n // bn)
             for sk in (1, 2, 4, 8):
                 if G._pp_valid(cfg, n, k, mode, sk) and (sk == 1 or (tiles < 256 and tiles * sk <= 1024)) \
                         and (cfg, sk) not in out:
@@ -166,7 +188,7 @@ def main():
                     cands = [("gemv", 1)]
                 else:
                     cands = (skinny_candidates(m, n, k, mode) if m <= G.SKINNY_MAX_M else []) + \
-                        (candidates(m, n, k, mode) if m >= 16 else [])
+                        (candidates(m, n, k, mode) if m >= 16 else tiny_candidates(m, n, k, mode))
                 ref = lib(0).float()
                 scale = ref.abs().max().item() + 1e-6
                 bad = [c for c in cands if (own(0, c).float() - ref).abs().max().item() > 0.03 * scale]

@@ -35,7 +35,7 @@ def _check(y, ref, tol=2e-2):
     assert err <= tol * scale, f"max err {err:.4g} vs max |ref| {scale:.4g}"
 
 
-LG = [12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 38, 39]
+LG = [12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 38, 39, 72, 73, 74, 75]
 # gemm_lg.hip configs (12-19 / 29-31 ring schedule, 20-28 slab schedule, 32-39 mid-M weight streaming)
 CFGS = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11] + LG
 
@@ -63,7 +63,7 @@ def test_n_tail(cfg):
 
 
 @pytest.mark.parametrize("cfg,splitk", [(0, 2), (1, 4), (3, 2), (2, 5), (4, 2), (5, 4), (7, 2), (8, 2), (9, 4), (10, 2), (11, 5),
-                                        (12, 2), (13, 4), (14, 5), (15, 2), (16, 2), (17, 4), (18, 5), (19, 2), (20, 2), (21, 4), (22, 5), (23, 2), (24, 2), (25, 4), (26, 2), (27, 4), (28, 5), (29, 2), (30, 4), (31, 5), (32, 4), (33, 5), (34, 2), (35, 4), (36, 4), (37, 2), (38, 5), (39, 2)])
+                                        (12, 2), (13, 4), (14, 5), (15, 2), (16, 2), (17, 4), (18, 5), (19, 2), (20, 2), (21, 4), (22, 5), (23, 2), (24, 2), (25, 4), (26, 2), (27, 4), (28, 5), (29, 2), (30, 4), (31, 5), (32, 4), (33, 5), (34, 2), (35, 4), (36, 4), (37, 2), (38, 5), (39, 2), (72, 4), (73, 2), (74, 5), (75, 4)])
 def test_splitk(cfg, splitk):
     g = torch.Generator(device=DEV).manual_seed(11 + cfg)
     m, n, k = 300, 512, 64 * 20
@@ -95,7 +95,7 @@ def test_swiglu_normp(cfg):
 
 
 @pytest.mark.parametrize("cfg,splitk", [(0, 1), (1, 2), (3, 1), (4, 1), (5, 2), (8, 1), (9, 2), (10, 1),
-                                        (12, 1), (12, 2), (13, 1), (14, 2), (15, 1), (16, 1), (17, 2), (18, 1), (19, 2), (20, 1), (20, 2), (21, 1), (22, 2), (23, 1), (24, 1), (24, 2), (25, 1), (26, 1), (26, 2), (27, 1), (28, 2), (29, 1), (30, 2), (31, 1), (32, 1), (32, 4), (33, 2), (34, 1), (35, 2), (36, 4), (37, 1), (38, 2), (39, 1)])
+                                        (12, 1), (12, 2), (13, 1), (14, 2), (15, 1), (16, 1), (17, 2), (18, 1), (19, 2), (20, 1), (20, 2), (21, 1), (22, 2), (23, 1), (24, 1), (24, 2), (25, 1), (26, 1), (26, 2), (27, 1), (28, 2), (29, 1), (30, 2), (31, 1), (32, 1), (32, 4), (33, 2), (34, 1), (35, 2), (36, 4), (37, 1), (38, 2), (39, 1), (72, 2), (73, 1), (75, 2)])
 def test_resid_partials(cfg, splitk):
     g = torch.Generator(device=DEV).manual_seed(5 + cfg)
     m, n, k = 259, 512, 768
