@@ -17,6 +17,8 @@ struct PPArgs {
     int M, N, K, F, nparts_in, splitk, kts;
     float eps;
     int gm;      // tile order: M-tiles per group (0 = every M-tile of a W panel consecutive); knob pp_gm
+    const float* xsc;  // gemm_lg F8 (W8A8 e4m3fn bytes in x / w): per-token scales [M]
+    const float* wsc;  // ... and per-output-channel scales [N]
     int ablate;  // timing-only diagnostics (knob pp_ablate): 1 skip loop DMA, 2 skip LDS reads, 4 skip MFMA, 8 nt weights, 16/32 alias every W/x tile onto tile 0
 };
 
@@ -34,6 +36,11 @@ constexpr int kLGTinyFirst = 72, kLGTinyConfigs = 4;  // gemm_lg 72-75 (after th
 int gemm_lg_xm(int cfg);  // x rows per tile
 int gemm_lg_wn(int cfg);  // W rows per tile
 bool launch_gemm_lg(int cfg, int mode, bool normp, const PPArgs& a, hipStream_t st);
+// W8A8 fp8 configs of the same kernel (ring schedule, 128-deep stages; a.kts counts 128-deep units), own id space
+constexpr int kLGF8Configs = 4;
+int gemm_lg_f8_xm(int cfg);
+int gemm_lg_f8_wn(int cfg);
+bool launch_gemm_lg_f8(int cfg, bool swiglu, const PPArgs& a, hipStream_t st);
 
 // skinny-M family (csrc/kernels/gemm_skinny.hip, M <= 16 * MT): same PPArgs / epilogues; the workgroup owns 16 * RT
 // W rows (swiglu: 8 * RT gate + 8 * RT up), ws holds [groups * splitk, 64 * RT * MT] f32x4 slabs, cnt one ticket per

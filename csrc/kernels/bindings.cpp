@@ -666,6 +666,50 @@ Tensor qlinear(const Tensor& xq, const Tensor& xs, const Tensor& wq, const Tenso
     return y;
 }
 
+// W8A8 on gemm_lg.hip's ring schedule (fp8 configs, gemm_lg_f8_*): the same result as qlinear for M >= 256 shapes.
+// splitk divides K / 128.
+Tensor qgemm_lg(const Tensor& xq, const Tensor& xs, const Tensor& wq, const Tensor& ws, bool swiglu, int64_t cfg,
+                int64_t splitk) {
+    chk_gpu(xq, "xq");
+    chk_gpu(wq, "wq");
+    chk_gpu(xs, "xs");
+    chk_gpu(ws, "ws");
+    CHK(xq.scalar_type() == at::kByte && wq.scalar_type() == at::kByte, "qgemm_lg: xq / wq must be uint8 (e4m3fn)");
+    CHK(xs.scalar_type() == at::kFloat && ws.scalar_type() == at::kFloat, "qgemm_lg: scales must be f32");
+    CHK(cfg >= 0 && cfg < chronos::kLGF8Configs, "qgemm_lg: cfg");
+    const int64_t K = xq.size(-1), M = xq.numel() / K, N = wq.size(0);
+    const int BM = chronos::gemm_lg_f8_xm((int)cfg), BN = chronos::gemm_lg_f8_wn((int)cfg);
+    CHK(wq.dim() == 2 && wq.size(1) == K, "qgemm_lg: wq must be [N, K]");
+    CHK(xs.numel() == M && ws.numel() == N, "qgemm_lg: one scale per token row / weight row");
+    CHK(K % 128 == 0 && K <= (1 << 20) && splitk >= 1 && (K / 128) % splitk == 0, "qgemm_lg: splitk must divide K / 128");
+    CHK(swiglu ? N % BN == 0 : N % 4 == 0, "qgemm_lg: N % 4 (plain) / N % BN (swiglu)");
+    CHK(M >= 1 && (N + BN) * K < (1LL << 31) && (M + BM) * K < (1LL << 31), "qgemm_lg: operand > 2 GiB");
+    c10::hip::HIPGuardMasqueradingAsCUDA g(xq.device());
+    chronos::PPArgs a{};
+    a.x = reinterpret_cast<const uint16_t*>(xq.data_ptr<uint8_t>());
+    a.w = reinterpret_cast<const uint16_t*>(wq.data_ptr<uint8_t>());
+    a.xsc = xs.data_ptr<float>();
+    a.wsc = ws.data_ptr<float>();
+    a.M = (int)M;
+    a.N = (int)N;
+    a.K = (int)K;
+    a.F = (int)(N / 2);
+    a.splitk = (int)splitk;
+    a.kts = (int)(K / 128 / splitk);
+    a.gm = chronos::knob("pp_gm", 8);
+    Tensor y = at::empty({M, swiglu ? N / 2 : N}, xq.options().dtype(at::kBFloat16));
+    a.y = bfm(y);
+    const int64_t tiles = ((M + BM - 1) / BM) * (swiglu ? (N / 2) / (BN / 2) : (N + BN - 1) / BN);
+    Tensor wsl;
+    if (splitk > 1) {
+        wsl = at::empty({tiles * splitk * BM * BN}, xs.options());
+        a.ws = wsl.data_ptr<float>();
+        a.cnt = split_tickets(xq, tiles);
+    }
+    CHK(chronos::launch_gemm_lg_f8((int)cfg, swiglu, a, cur_stream()), "qgemm_lg: launch");
+    return y;
+}
+
 // value < 0: forget the setting (the next read takes CHRONOS_<NAME> or the built-in default again)
 void set_knob(const std::string& name, int64_t value) {
     std::lock_guard<std::mutex> lk(chronos::g_knob_mu);
@@ -745,6 +789,7 @@ TORCH_LIBRARY(chronos, m) {
     m.def("attn_init() -> ()", [] { chronos::attn_init(); });
     m.def("quant_rows(Tensor x, Tensor(a!)? resid, Tensor? w, float eps, int mode) -> (Tensor, Tensor)");
     m.def("qlinear(Tensor xq, Tensor xs, Tensor wq, Tensor ws, bool swiglu) -> Tensor");
+    m.def("qgemm_lg(Tensor xq, Tensor xs, Tensor wq, Tensor ws, bool swiglu, int cfg, int splitk) -> Tensor");
     m.def("set_knob(str name, int value) -> ()", &set_knob);
     m.def("ar_create(int rank, int world, int max_bytes) -> int", &ar_create);
     m.def("ar_handles(int h) -> Tensor", &ar_handles);
@@ -780,6 +825,7 @@ TORCH_LIBRARY_IMPL(chronos, CUDA, m) {
     m.impl("qkv_rope", &qkv_rope);
     m.impl("quant_rows", &quant_rows);
     m.impl("qlinear", &qlinear);
+    m.impl("qgemm_lg", &qgemm_lg);
     m.impl("paged_attention", &paged_attention);
     m.impl("decode_attention_rope", &decode_attention_rope);
     m.impl("constrained_sample", &constrained_sample);

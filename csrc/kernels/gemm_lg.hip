@@ -96,6 +96,16 @@ __device__ __forceinline__ void lg_dma16_asm(const void* base, int bytes, uint32
                  ::"v"(voff), "s"(r), "s"(lds), "s"(soff) : "memory");
 }
 
+// W8A8 fp8 (F8): a fragment of v_mfma_scale_f32_16x16x128_f8f6f4 is 32 k-bytes per lane (two 16-B chunks)
+typedef int lg_i32x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ f32x4 lg_mma(const bf16x8& a, const bf16x8& b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// block-scaled form fed the unit MX exponent (127 = 2^0): the per-token / per-channel scales go in the epilogue
+__device__ __forceinline__ f32x4 lg_mma(const lg_i32x8& a, const lg_i32x8& b, f32x4 c) {
+    return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
+}
+
 // 64-B-row chunk swizzle (the 16x16x32 fragment reads of a 16-row block land on 16 distinct 16-B slots)
 __device__ __forceinline__ int lg_swz64(int row) { return (4 - ((row >> 2) & 3)) & 3; }
 
@@ -108,12 +118,18 @@ __device__ __forceinline__ int lg_swz64(int row) { return (4 - ((row >> 2) & 3))
 // ds_read), 1 STG, 2 MAN: each k-step written out in issue order, DMA pieces as inline-asm buffer_load ... lds spread
 // evenly through k-step B among the MFMAs and ds_reads (hipcc cannot see an asm DMA write LDS, so it adds no
 // lgkmcnt wait in front of it; the ring buffers it writes are disjoint from the ones being read by construction)
-template <int WN, int XM, int RB, int ST, int MODE, bool NORMP, int NWX, int ABL = 0, int VAR = 0>
+// F8 (ring schedule only): W8A8 e4m3fn operands (PPArgs x / w hold the bytes), one 128-deep MFMA k-step per 128-B
+// stage row, y = (x W^T) * xsc[m] * wsc[n] in the epilogue (plain / SwiGLU)
+template <int WN, int XM, int RB, int ST, int MODE, bool NORMP, int NWX, int ABL = 0, int VAR = 0, bool F8 = false>
 __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
     constexpr bool STG = VAR == 1, MAN = VAR == 2;
+    constexpr int ES = F8 ? 1 : 2;  // operand bytes per element
+    static_assert(!F8 || (ST >= 3 && RB == 128 && MODE != kResid && !NORMP && VAR == 0 && ABL == 0),
+                  "fp8: ring schedule, 128-B rows, plain / SwiGLU epilogue");
+    using FT = std::conditional_t<F8, lg_i32x8, bf16x8>;  // MFMA operand fragment
     constexpr int NW = 2 * NWX;                       // waves: 2 along W x NWX along x (NWX = 4: two per SIMD)
     constexpr int RPI = 1024 / RB;                    // image rows per LDS-DMA instruction
-    constexpr int KS = RB / 64;                       // 32-deep k-steps per stage
+    constexpr int KS = F8 ? 1 : RB / 64;              // MFMA k-steps per stage (bf16 32 deep, F8 128 deep)
     constexpr int WIMG = WN * RB, XIMG = XM * RB, STAGE = WIMG + XIMG;
     constexpr int NINS = (WN + XM) / RPI;             // DMA instructions per stage (whole workgroup)
     constexpr int NPER = NINS / NW;                   // ... per wave
@@ -154,15 +170,16 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
     }
     const int m0 = tm * XM;
     const int tns = (ABL & 8) ? 0 : tn, m0s = (ABL & 8) ? 0 : m0;  // DMA source tile (diagnostics may alias)
-    const int NS = a.kts * (64 / (RB / 2));           // stages of this task's K range (kts = 64-deep units)
-    const int64_t kbeg = (int64_t)ks * a.kts * 64;
+    // stages of this task's K range: kts = 64-deep units (bf16) / 128-deep units (F8, one per stage)
+    const int NS = F8 ? a.kts : a.kts * (64 / (RB / 2));
+    const int64_t kbeg = (int64_t)ks * a.kts * (F8 ? 128 : 64);
 
     // ---- LDS-DMA sources: instruction q of the stage (q = wave * NPER + i) fills image rows q*RPI .. +RPI of the
     // concatenated [W rows; x rows] image; lane l fills row q*RPI + l / (RB/16), physical chunk l % (RB/16), from the
     // logical chunk the read-side swizzle maps there.  buffer_load ... lds through one descriptor per operand: a 32-bit
     // per-lane byte offset (half the VGPRs of flat 64-bit addresses), the stage's k offset in the scalar soffset, and
     // rows past the end of W / x (partial last tiles) read as zeros by the descriptor's range check (never stored)
-    const int wbytes = (int)((MODE == kSwiglu ? 2 * a.F : a.N) * (int64_t)K * 2), xbytes = (int)((int64_t)M * K * 2);
+    const int wbytes = (int)((MODE == kSwiglu ? 2 * a.F : a.N) * (int64_t)K * ES), xbytes = (int)((int64_t)M * K * ES);
     uint32_t voff[NPER];
     int dsto[NPER];
     bool isw[NPER];
@@ -180,11 +197,11 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
             else
                 wrow = tns * WN + r;
             const int lc = RB == 64 ? pc ^ lg_swz64(r) : pc ^ (r & 7);
-            voff[i] = (uint32_t)(((int64_t)wrow * K + kbeg + lc * 8) * 2);
+            voff[i] = (uint32_t)(((int64_t)wrow * K + kbeg) * ES + lc * 16);
         } else {
             const int xr = r - WN;
             const int lc = RB == 64 ? pc ^ lg_swz64(xr) : pc ^ (xr & 7);
-            voff[i] = (uint32_t)(((int64_t)(m0s + xr) * K + kbeg + lc * 8) * 2);
+            voff[i] = (uint32_t)(((int64_t)(m0s + xr) * K + kbeg) * ES + lc * 16);
         }
     }
     // DMA of stage j into ring buffer j % ST.  Issued unconditionally so it shares a basic block with the MFMAs it is
@@ -209,10 +226,13 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
             wrow0[s] = wi * (WN / 2) + 16 * s;
     }
     const int xrow0 = wj * (XM / NWX);
-    int loff[KS];
+    // F8: the two chunks 2 (lane >> 4) and 2 (lane >> 4) + 1 of the lane's 128-B row, swizzled like the bf16 reads
+    int loff[F8 ? 2 : KS];
 #pragma unroll
-    for (int kk = 0; kk < KS; ++kk) {
-        if constexpr (RB == 64)
+    for (int kk = 0; kk < (F8 ? 2 : KS); ++kk) {
+        if constexpr (F8)
+            loff[kk] = (lane & 15) * 128 + (((2 * (lane >> 4) + kk) ^ (lane & 7)) << 4);
+        else if constexpr (RB == 64)
             loff[kk] = (lane & 15) * 64 + (((lane >> 4) ^ lg_swz64(lane & 15)) << 4);
         else
             loff[kk] = (lane & 15) * 128 + (((4 * kk + (lane >> 4)) ^ (lane & 7)) << 4);
@@ -402,24 +422,33 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
     lg_vmcnt<(ST - 2) * NPER>();
     lg_bar();
 
-    bf16x8 fa0[NA], fb0[NB], fa1[NA], fb1[NB];
-    auto read_frags = [&](int j, bf16x8 (&fa)[NA], bf16x8 (&fb)[NB]) {
+    FT fa0[NA], fb0[NB], fa1[NA], fb1[NB];
+    // one fragment of the 16-row block starting at LDS row pointer p (F8: two ds_read_b128)
+    auto frag = [&](const unsigned char* p, int kk) -> FT {
+        if constexpr (F8) {
+            typedef int i32x4_t __attribute__((ext_vector_type(4)));
+            const i32x4_t lo = *reinterpret_cast<const i32x4_t*>(p + loff[0]);
+            const i32x4_t hi = *reinterpret_cast<const i32x4_t*>(p + loff[1]);
+            return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        } else {
+            return *reinterpret_cast<const bf16x8*>(p + loff[kk]);
+        }
+    };
+    auto read_frags = [&](int j, FT (&fa)[NA], FT (&fb)[NB]) {
         const unsigned char* wb = smem + (j % ST) * STAGE;
         const unsigned char* xb = wb + WIMG;
 #pragma unroll
         for (int kk = 0; kk < KS; ++kk) {
 #pragma unroll
-            for (int s = 0; s < NT; ++s)
-                fa[kk * NT + s] = *reinterpret_cast<const bf16x8*>(wb + wrow0[s] * RB + loff[kk]);
+            for (int s = 0; s < NT; ++s) fa[kk * NT + s] = frag(wb + wrow0[s] * RB, kk);
 #pragma unroll
-            for (int t = 0; t < MT; ++t)
-                fb[kk * MT + t] = *reinterpret_cast<const bf16x8*>(xb + (xrow0 + 16 * t) * RB + loff[kk]);
+            for (int t = 0; t < MT; ++t) fb[kk * MT + t] = frag(xb + (xrow0 + 16 * t) * RB, kk);
         }
     };
     read_frags(0, fa0, fb0);
 
     // one K stage; the fragments of stage t are in (fa, fb), stage t+1's are read into (na, nb)
-    auto stage = [&](int t, bf16x8 (&fa)[NA], bf16x8 (&fb)[NB], bf16x8 (&na)[NA], bf16x8 (&nb)[NB]) {
+    auto stage = [&](int t, FT (&fa)[NA], FT (&fb)[NB], FT (&na)[NA], FT (&nb)[NB]) {
         // part 1: DMA of stage t+ST-1 || MFMAs over W blocks [0, H1)
         if constexpr (!(ABL & 1)) issue(t + ST - 1);
         if constexpr (!(ABL & 4)) {
@@ -428,9 +457,7 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
 #pragma unroll
                 for (int s = 0; s < H1; ++s)
 #pragma unroll
-                    for (int u = 0; u < MT; ++u)
-                        acc[s][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk * NT + s], fb[kk * MT + u],
-                                                                            acc[s][u], 0, 0, 0);
+                    for (int u = 0; u < MT; ++u) acc[s][u] = lg_mma(fa[kk * NT + s], fb[kk * MT + u], acc[s][u]);
         } else {
 #pragma unroll
             for (int i = 0; i < NA; ++i) asm volatile("" ::"v"(fa[i]));
@@ -461,12 +488,10 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
 #pragma unroll
                 for (int s = H1; s < NT; ++s)
 #pragma unroll
-                    for (int u = 0; u < MT; ++u)
-                        acc[s][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kk * NT + s], fb[kk * MT + u],
-                                                                            acc[s][u], 0, 0, 0);
+                    for (int u = 0; u < MT; ++u) acc[s][u] = lg_mma(fa[kk * NT + s], fb[kk * MT + u], acc[s][u]);
         }
         {
-            constexpr int NR = NA + NB;
+            constexpr int NR = (NA + NB) * (F8 ? 2 : 1);  // ds_read_b128 per stage
             constexpr int G = MF2 / NR > 0 ? MF2 / NR : 1;
 #pragma unroll
             for (int i = 0; i < NR; ++i) {
@@ -529,18 +554,24 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
         const int m = m0 + r;
         float sc = 1.f;
         if constexpr (NORMP) sc = inv[r];
+        if constexpr (F8) sc = m < M ? a.xsc[m] : 0.f;  // per-token scale; the per-channel one below
         if constexpr (MODE == kSwiglu) {
             if (m < M) {
 #pragma unroll
                 for (int s = 0; s < NT / 2; ++s) {
+                    const int f = tn * (WN / 2) + wrow0[s] + 4 * (lane >> 4);
+                    f32x4 cg = {1.f, 1.f, 1.f, 1.f}, cu = {1.f, 1.f, 1.f, 1.f};
+                    if constexpr (F8) {
+                        cg = *reinterpret_cast<const f32x4*>(a.wsc + f);
+                        cu = *reinterpret_cast<const f32x4*>(a.wsc + a.F + f);
+                    }
                     u16x4 o;
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
-                        const float gv = bf2f(f2bf(acc[s][u][i] * sc));
+                        const float gv = bf2f(f2bf(acc[s][u][i] * sc * cg[i]));
                         const float sg = bf2f(f2bf(gv / (1.f + __expf(-gv))));
-                        o[i] = f2bf(sg * bf2f(f2bf(acc[s + NT / 2][u][i] * sc)));
+                        o[i] = f2bf(sg * bf2f(f2bf(acc[s + NT / 2][u][i] * sc * cu[i])));
                     }
-                    const int f = tn * (WN / 2) + wrow0[s] + 4 * (lane >> 4);
                     *reinterpret_cast<u16x4*>(a.y + (int64_t)m * a.F + f) = o;
                 }
             }
@@ -569,10 +600,13 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
             if (m < M) {
 #pragma unroll
                 for (int s = 0; s < NT; ++s) {
+                    const int n = tn * WN + wrow0[s] + 4 * (lane >> 4);
+                    f32x4 cw = {1.f, 1.f, 1.f, 1.f};
+                    if constexpr (F8)
+                        if (n < a.N) cw = *reinterpret_cast<const f32x4*>(a.wsc + n);
                     u16x4 o;
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) o[i] = f2bf(acc[s][u][i] * sc);
-                    const int n = tn * WN + wrow0[s] + 4 * (lane >> 4);
+                    for (int i = 0; i < 4; ++i) o[i] = f2bf(acc[s][u][i] * sc * cw[i]);
                     if (n < a.N) *reinterpret_cast<u16x4*>(a.y + (int64_t)m * a.N + n) = o;  // N % 4 == 0
                 }
             }
@@ -580,10 +614,10 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
     }
 }
 
-template <int WN, int XM, int RB, int ST, int MODE, bool NORMP, int NWX, int ABL = 0, int VAR = 0>
+template <int WN, int XM, int RB, int ST, int MODE, bool NORMP, int NWX, int ABL = 0, int VAR = 0, bool F8 = false>
 void lg_launch(const PPArgs& a, hipStream_t st) {
     const int lds = ST * (WN + XM) * RB + 16 + XM * 4;
-    auto kern = gemm_lg_kernel<WN, XM, RB, ST, MODE, NORMP, NWX, ABL, VAR>;
+    auto kern = gemm_lg_kernel<WN, XM, RB, ST, MODE, NORMP, NWX, ABL, VAR, F8>;
     static bool attr = false;
     if (!attr) {
         hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
@@ -692,6 +726,49 @@ int gemm_lg_wn(int cfg) {
 #undef LG_WN
         default: return 0;
     }
+}
+
+// W8A8 fp8 configs {id, WN, XM, RB, ST, NWX}: ring schedule, one 128-deep v_mfma_scale_f32_16x16x128_f8f6f4 k-step
+// per 128-B stage row (every staged byte carries twice the bf16 kernel's K)
+#define LG_F8_CONFIGS(X)       \
+    X(0, 256, 128, 128, 3, 4)  \
+    X(1, 128, 256, 128, 3, 4)  \
+    X(2, 128, 128, 128, 4, 2)  \
+    X(3, 128, 128, 128, 3, 4)
+
+namespace {
+template <int MODE>
+bool lg_f8_mode(int cfg, const PPArgs& a, hipStream_t st) {
+    switch (cfg) {
+#define LG_F8_CASE(ID, WN_, XM_, RB_, ST_, NWX_) \
+    case ID: lg_launch<WN_, XM_, RB_, ST_, MODE, false, NWX_, 0, 0, true>(a, st); return true;
+        LG_F8_CONFIGS(LG_F8_CASE)
+#undef LG_F8_CASE
+        default: return false;
+    }
+}
+}  // namespace
+
+int gemm_lg_f8_xm(int cfg) {
+    switch (cfg) {
+#define LG_F8_XM(ID, WN_, XM_, RB_, ST_, NWX_) case ID: return XM_;
+        LG_F8_CONFIGS(LG_F8_XM)
+#undef LG_F8_XM
+        default: return 0;
+    }
+}
+int gemm_lg_f8_wn(int cfg) {
+    switch (cfg) {
+#define LG_F8_WN(ID, WN_, XM_, RB_, ST_, NWX_) case ID: return WN_;
+        LG_F8_CONFIGS(LG_F8_WN)
+#undef LG_F8_WN
+        default: return 0;
+    }
+}
+
+bool launch_gemm_lg_f8(int cfg, bool swiglu, const PPArgs& a, hipStream_t st) {
+    if (a.M == 0) return true;
+    return swiglu ? lg_f8_mode<kSwiglu>(cfg, a, st) : lg_f8_mode<kPlain>(cfg, a, st);
 }
 
 bool launch_gemm_lg(int cfg, int mode, bool normp, const PPArgs& a, hipStream_t st) {

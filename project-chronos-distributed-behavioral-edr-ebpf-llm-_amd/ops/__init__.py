@@ -140,6 +140,11 @@ def qlinear(xq: torch.Tensor, xs: torch.Tensor, wq: torch.Tensor, ws: torch.Tens
     if xq.is_cuda:
         m, k = xq.numel() // xq.shape[-1], xq.shape[-1]
         if _qown(m, wq.shape[0], k, swiglu):
+            from .gemm import QLG_BASE, qplan_route
+
+            r = qplan_route(m, wq.shape[0], k, swiglu) if _QGEMM == "auto" else None
+            if r is not None and r[0] >= QLG_BASE:  # gemm_lg.hip fp8 config (the large-M ring schedule)
+                return _k().qgemm_lg(xq, xs, wq, ws, swiglu, r[0] - QLG_BASE, r[1])
             return _k().qlinear(xq, xs, wq, ws, swiglu)
         y = _qlib(xq, xs, wq, ws)
         return silu_mul(y) if swiglu else y

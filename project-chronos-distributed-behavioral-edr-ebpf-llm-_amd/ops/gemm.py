@@ -78,16 +78,26 @@ def _plan_file() -> dict:
     return _plan_table
 
 
-def qplan_own(m: int, n: int, k: int, swiglu: bool) -> Optional[bool]:
-    """W8A8 fp8 projection: True = the hand-written kernels (fp8.hip qgemv / block-scaled MFMA qgemm), False = the
-    library's fp8 GEMM, None = not measured.  Rows [measured M, 1 own / 0 library] per (N, K, swiglu) from
-    ``scripts/tune_gemm_pp.py --fp8``, read like the bf16 plan's."""
+QLG_BASE = 10  # qplan code >= QLG_BASE: gemm_lg.hip's fp8 config (code - QLG_BASE), row [M, code, split-K]
+QLG_GEO = {0: (128, 256), 1: (256, 128), 2: (128, 128), 3: (128, 128)}  # fp8 config -> (x rows, W rows) per tile
+
+
+def qplan_route(m: int, n: int, k: int, swiglu: bool) -> Optional[tuple[int, int]]:
+    """W8A8 fp8 projection route from ops/gemm_plan.json "qplans" (``scripts/tune_gemm_pp.py --fp8``), rows
+    [measured M, code(, split-K)] per (N, K, swiglu) read like the bf16 plan's: code 0 = the library's fp8 GEMM, 1 =
+    fp8.hip (qgemv / block-scaled MFMA qgemm), QLG_BASE + c = gemm_lg.hip fp8 config c.  None = not measured."""
     _plan_file()
     rows = (_qplan_table or {}).get((n, k, int(swiglu)))
     if not rows:
         return None
     pick = next((r for r in rows if m <= r[0]), rows[-1])
-    return bool(pick[1])
+    return int(pick[1]), int(pick[2]) if len(pick) > 2 else 1
+
+
+def qplan_own(m: int, n: int, k: int, swiglu: bool) -> Optional[bool]:
+    """True = a hand-written fp8 kernel (fp8.hip or gemm_lg.hip), False = the library, None = not measured."""
+    r = qplan_route(m, n, k, swiglu)
+    return None if r is None else r[0] != 0
 
 
 def _sk_valid(c: int, m: int, n: int, k: int, mode: int, sk: int) -> bool:

@@ -253,7 +253,9 @@ def tune_fp8(args, merged_unused):
     """W8A8: the hand-written fp8 kernels (qgemv / block-scaled MFMA qgemm, fused SwiGLU) against hipBLASLt's fp8 GEMM
     (+ silu_mul for gate_up), per 8B projection shape and M; rows [M, 1 own / 0 library] -> "qplans"."""
     from chronos import ops
+    from chronos.ops import gemm as G
 
+    G_F8 = G.QLG_GEO
     dev = "cuda"
     ms = [int(v) for v in args.ms.split(",")]
     st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -276,18 +278,34 @@ def tune_fp8(args, merged_unused):
             def own(i):
                 return torch.ops.chronos.qlinear(xq, xs, wqs[i % ncopy], wsc, swiglu)
 
+            # gemm_lg.hip's fp8 configs (M >= 128): every config that tiles N, split-K while the grid under-fills
+            lgc = []
+            if m >= 128:
+                for c in range(4):
+                    bm, bn = G_F8[c]
+                    tiles = -(-m // bm) * (n // bn)
+                    for sk in (1, 2, 4):
+                        if (n % bn == 0) and (k // 128) % sk == 0 and (sk == 1 or tiles * sk <= 768):
+                            lgc.append((c, sk))
+
             def lib(i):
                 y = ops._qlib(xq, xs, wqs[i % ncopy], wsc)
                 return ops.silu_mul(y) if swiglu else y
 
             ref = lib(0).float()
-            err = (own(0).float() - ref).abs().max().item()
-            assert err <= 0.03 * (ref.abs().max().item() + 1e-6), f"fp8 {op} M={m}: err {err}"
+            fns = {"lib": lib, "own": own}
+            for c, sk in lgc:
+                fns[f"lg{c}_sk{sk}"] = (lambda c_, sk_: lambda i: torch.ops.chronos.qgemm_lg(
+                    xq, xs, wqs[i % ncopy], wsc, swiglu, c_, sk_))(c, sk)
+            for name, fn in fns.items():
+                if name != "lib":
+                    err = (fn(0).float() - ref).abs().max().item()
+                    assert err <= 0.03 * (ref.abs().max().item() + 1e-6), f"fp8 {op} M={m} {name}: err {err}"
             flop = 2.0 * m * n * k
             iters = max(2, min(args.iters, int(4e13 / flop) + 2))
-            t = {"own": [], "lib": []}
+            t = {name: [] for name in fns}
             for _ in range(args.rounds):
-                for name, fn in (("lib", lib), ("own", own)):
+                for name, fn in fns.items():
                     fn(0)
                     torch.cuda.synchronize()
                     st.record()
@@ -296,13 +314,22 @@ def tune_fp8(args, merged_unused):
                     en.record()
                     torch.cuda.synchronize()
                     t[name].append(st.elapsed_time(en) * 1000 / iters)
-            own_us, lib_us = min(t["own"]), min(t["lib"])
+            best = min((v for v in t if v != "lib"), key=lambda v: min(t[v]))
+            own_us, lib_us = min(t[best]), min(t["lib"])
             use_own = not lib_us < own_us / 1.03
-            rows.append([m, int(use_own)])
+            if not use_own:
+                rows.append([m, 0])
+            elif best == "own":
+                rows.append([m, 1])
+            else:
+                c, sk = (int(v) for v in best[2:].split("_sk"))
+                rows.append([m, G.QLG_BASE + c, sk])
             rec = dict(model="8b-fp8", op=op, m=m, n=n, k=k, mode=mode, lib_us=round(lib_us, 2),
-                       own_us=round(own_us, 2), own="fp8.hip", lib_TF=round(flop / lib_us / 1e6, 1),
+                       own_us=round(own_us, 2), own="fp8.hip" if best == "own" else "gemm_lg fp8 " + best,
+                       lib_TF=round(flop / lib_us / 1e6, 1),
                        own_TF=round(flop / own_us / 1e6, 1), own_weight_TBs=round(n * k / own_us / 1e6, 2),
-                       speedup=round(lib_us / own_us, 3), route="own" if use_own else "lib", all={})
+                       speedup=round(lib_us / own_us, 3), route="own" if use_own else "lib",
+                       all={v: round(min(ts), 2) for v, ts in t.items()})
             table.append(rec)
             print(json.dumps(rec), flush=True)
         if rows:

@@ -157,3 +157,40 @@ def test_fp8_model_tracks_bf16_and_engine_valid():
     eng.run_until_idle()
     for r in reqs:
         assert {"risk_score", "verdict", "reason"} <= set(json.loads(r.text))
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("m,n,k,swiglu,splitk", [(300, 2048, 2048, False, 1), (257, 1024, 4096, True, 1),
+                                                 (130, 2052, 1024, False, 2), (77, 512, 2048, True, 4)])
+def test_qgemm_lg(cfg, m, n, k, swiglu, splitk):
+    """gemm_lg.hip's fp8 configs (ring schedule, one v_mfma_scale_f32_16x16x128_f8f6f4 k-step per 128-B stage) against
+    the fp32 reference: partial M and N tiles (N % 4 only, plain), SwiGLU, split-K (tickets left at zero: 3 calls)."""
+    from chronos.ops import reference as ref
+
+    g = torch.Generator(device=DEV).manual_seed(cfg * 31 + m + n + k)
+    xq, xs, wq, ws = _qpair(m, n, k, g, swiglu)
+    yr = ref.qlinear(xq, xs, wq, ws, swiglu)
+    tol = dict(rtol=2e-2, atol=2e-2 * float(yr.float().abs().mean()) + 1e-6)
+    for _ in range(3):
+        y = torch.ops.chronos.qgemm_lg(xq, xs, wq, ws, swiglu, cfg, splitk)
+        assert y.shape == yr.shape
+        torch.testing.assert_close(y.float(), yr.float(), **tol)
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+def test_qgemm_lg_onehot_layout(cfg):
+    """One-hot x rows (exact in e4m3): pins the fp8 fragment layout (row, column, k of every lane's 32 bytes)."""
+    from chronos.ops import reference as ref
+
+    m, k, n = 300, 2048, 512
+    g = torch.Generator(device=DEV).manual_seed(cfg)
+    cols = torch.randint(0, k, (m,), device=DEV, generator=g)
+    xq = torch.zeros(m, k, dtype=torch.float8_e4m3fn, device=DEV)
+    xq[torch.arange(m, device=DEV), cols] = 1.0
+    xq = xq.view(torch.uint8)
+    xs = torch.rand(m, device=DEV, generator=g) + 0.5
+    w = torch.randn(n, k, device=DEV, generator=g).to(torch.bfloat16)
+    wq, ws = ref.quantize_weight(w)
+    y = torch.ops.chronos.qgemm_lg(xq, xs, wq, ws, False, cfg, 1)
+    want = (_deq(wq, ws)[:, cols].t() * xs[:, None]).to(torch.bfloat16)
+    torch.testing.assert_close(y.float(), want.float(), rtol=1e-2, atol=1e-6)
