@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round-4 session-end GPU evidence: the whole GPU test suite, then smoke() (both as the driver runs them)
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+O=gpurun_out/final4
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1
+rc=$?
+tail -3 $O/pytest_gpu.log
+[ $rc -eq 0 ] || { grep -m5 "FAILED\|Error" $O/pytest_gpu.log; exit $rc; }
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
