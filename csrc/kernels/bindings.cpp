@@ -18,7 +18,6 @@
 #include <unordered_map>
 #include <vector>
 #include <cstring>
-#include <algorithm>
 
 #include "chronos_gemv.h"
 #include "chronos_gemm.h"
@@ -488,23 +487,6 @@ static int32_t* split_tickets(const Tensor& x, int64_t n) {
     return it->second.data_ptr<int32_t>();
 }
 
-// Stream-K geometry (gemm_lg): one workgroup per CU, each owning an even share of the tiles x units iterations; skmax
-// bounds the passes over one tile (its partial slabs)
-static void stream_k(chronos::PPArgs& a, int64_t tiles, int64_t units) {
-    static int cus = 0;
-    if (cus == 0) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        if (cus <= 0) cus = 256;
-    }
-    const int64_t I = tiles * units;
-    a.skg = (int)std::min<int64_t>(cus, I);
-    a.nslab = (int)units;
-    const int64_t per = std::max<int64_t>(1, I / a.skg);
-    a.skmax = (int)((units + per - 1) / per + 1);
-}
-
 // Batched projection GEMM family (gemm_pp.hip): y = x @ w.T with a fused epilogue, M >= 3.
 //   mode 0 plain (y [M, N]); 1 swiglu (w = [gate; up] [2F, K], y [M, F] = silu(x Wg^T) * (x Wu^T)); 2 resid (y = the
 //   new residual stream bf16(bf16(x @ w.T) + resid), second output = per-row partial sums of y^2 [M, N / (BN/4)]).
@@ -527,8 +509,7 @@ std::tuple<Tensor, Tensor> gemm_pp(const Tensor& x, const Tensor& w, int64_t mod
     // gemm_lg addresses both operands through buffer descriptors: 32-bit byte offsets, with one tile of slack
     CHK(!lg || ((N + BN) * K * 2 < (1LL << 31) && (M + BM) * K * 2 < (1LL << 31)), "gemm_lg: operand > 2 GiB");
     CHK(M >= 1 && M < (1LL << 31) / BM && K % 64 == 0 && K <= (1 << 20) && N * K < (1LL << 40), "gemm_pp: size");
-    // splitk == 0: stream-K (gemm_lg configs): one workgroup per CU walks an even share of tiles x K/64 units
-    CHK(splitk == 0 ? lg : splitk >= 1 && (K / 64) % splitk == 0, "gemm_pp: splitk must divide K / 64 (0: stream-K, gemm_lg)");
+    CHK(splitk >= 1 && (K / 64) % splitk == 0, "gemm_pp: splitk must divide K / 64");
     CHK(mode == 0 ? N % 4 == 0 : N % BN == 0, "gemm_pp: N % 4 (plain) / N % BN (swiglu, resid)");
     CHK(mode != 1 || (lg ? (BN / 4) % 16 == 0 : (BN / 8) % 16 == 0), "gemm_pp: swiglu needs BN >= 128 (gemm_lg: 64)");
     CHK(mode != 2 || !part_in.has_value(), "gemm_pp: resid mode has no norm prologue");
@@ -540,8 +521,8 @@ std::tuple<Tensor, Tensor> gemm_pp(const Tensor& x, const Tensor& w, int64_t mod
     a.N = (int)N;
     a.K = (int)K;
     a.F = (int)(N / 2);
-    a.splitk = splitk > 0 ? (int)splitk : 1;
-    a.kts = (int)(K / 64 / a.splitk);
+    a.splitk = (int)splitk;
+    a.kts = (int)(K / 64 / splitk);
     a.eps = (float)eps;
     a.ablate = chronos::knob("pp_ablate", 0);
     a.gm = chronos::knob("pp_gm", 8);  // +7-9 % at M = 16384 (profiles/r3_gemm_tile_order_m16384.jsonl)
@@ -566,11 +547,6 @@ std::tuple<Tensor, Tensor> gemm_pp(const Tensor& x, const Tensor& w, int64_t mod
     Tensor ws;
     if (splitk > 1) {
         ws = at::empty({tiles * splitk * BM * BN}, x.options().dtype(at::kFloat));
-        a.ws = ws.data_ptr<float>();
-        a.cnt = split_tickets(x, tiles);
-    } else if (splitk == 0) {
-        stream_k(a, tiles, K / 64);
-        ws = at::empty({tiles * a.skmax * BM * BN}, x.options().dtype(at::kFloat));
         a.ws = ws.data_ptr<float>();
         a.cnt = split_tickets(x, tiles);
     }
@@ -705,8 +681,7 @@ Tensor qgemm_lg(const Tensor& xq, const Tensor& xs, const Tensor& wq, const Tens
     const int BM = chronos::gemm_lg_f8_xm((int)cfg), BN = chronos::gemm_lg_f8_wn((int)cfg);
     CHK(wq.dim() == 2 && wq.size(1) == K, "qgemm_lg: wq must be [N, K]");
     CHK(xs.numel() == M && ws.numel() == N, "qgemm_lg: one scale per token row / weight row");
-    CHK(K % 128 == 0 && K <= (1 << 20) && (splitk == 0 || (splitk >= 1 && (K / 128) % splitk == 0)),
-        "qgemm_lg: splitk must divide K / 128 (0: stream-K)");
+    CHK(K % 128 == 0 && K <= (1 << 20) && splitk >= 1 && (K / 128) % splitk == 0, "qgemm_lg: splitk must divide K / 128");
     CHK(swiglu ? N % BN == 0 : N % 4 == 0, "qgemm_lg: N % 4 (plain) / N % BN (swiglu)");
     CHK(M >= 1 && (N + BN) * K < (1LL << 31) && (M + BM) * K < (1LL << 31), "qgemm_lg: operand > 2 GiB");
     c10::hip::HIPGuardMasqueradingAsCUDA g(xq.device());
@@ -719,8 +694,8 @@ Tensor qgemm_lg(const Tensor& xq, const Tensor& xs, const Tensor& wq, const Tens
     a.N = (int)N;
     a.K = (int)K;
     a.F = (int)(N / 2);
-    a.splitk = splitk > 0 ? (int)splitk : 1;
-    a.kts = (int)(K / 128 / a.splitk);
+    a.splitk = (int)splitk;
+    a.kts = (int)(K / 128 / splitk);
     a.gm = chronos::knob("pp_gm", 8);
     Tensor y = at::empty({M, swiglu ? N / 2 : N}, xq.options().dtype(at::kBFloat16));
     a.y = bfm(y);
@@ -728,11 +703,6 @@ Tensor qgemm_lg(const Tensor& xq, const Tensor& xs, const Tensor& wq, const Tens
     Tensor wsl;
     if (splitk > 1) {
         wsl = at::empty({tiles * splitk * BM * BN}, xs.options());
-        a.ws = wsl.data_ptr<float>();
-        a.cnt = split_tickets(xq, tiles);
-    } else if (splitk == 0) {
-        stream_k(a, tiles, K / 128);
-        wsl = at::empty({tiles * a.skmax * BM * BN}, xs.options());
         a.ws = wsl.data_ptr<float>();
         a.cnt = split_tickets(xq, tiles);
     }

@@ -130,8 +130,7 @@ def _pp_valid(cfg: int, n: int, k: int, mode: int, sk: int, m: int = 0) -> bool:
     if cfg >= SK_BASE:
         return cfg - SK_BASE in _SK and _sk_valid(cfg - SK_BASE, m, n, k, mode, sk)
     bn = _PP_BN[cfg]
-    # sk == 0: stream-K (gemm_lg configs only)
-    if k % 64 or (sk > 0 and (k // 64) % sk) or (sk == 0 and cfg < LG_FIRST):
+    if k % 64 or (k // 64) % sk:
         return False
     return n % 4 == 0 if mode == PP_PLAIN else n % bn == 0
 

@@ -43,11 +43,7 @@ def candidates(m, n, k, mode, cus=256):
         if n % BN[cfg]:
             continue
         tiles = -(-m // BM[cfg]) * (n // BN[cfg])
-        for sk in (0, 1, 2, 3, 4, 7, 8):  # 0: stream-K (gemm_lg configs)
-            if sk == 0:
-                if cfg >= 12 and cfg < 40 or cfg >= 72:
-                    out.append((cfg, 0))
-                continue
+        for sk in (1, 2, 3, 4, 7, 8):
             if (k // 64) % sk:
                 continue
             if sk > 1 and tiles * sk > 3 * cus:

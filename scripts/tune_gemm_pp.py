@@ -86,8 +86,6 @@ def candidates(m, n, k, mode, keep=6):
         for cfg in (20, 29, 30, 19, 31, 23):
             bm, bn = G._PP_BM[cfg], G._PP_BN[cfg]
             tiles = -(-m // bm) * -(-n // bn)
-            if tiles % 256 and m <= 4096 and G._pp_valid(cfg, n, k, mode, 0):
-                out.append((cfg, 0))  # stream-K: the tile count leaves part of the chip idle in the last round
             for sk in (1, 2, 4):
                 if G._pp_valid(cfg, n, k, mode, sk) and (sk == 1 or (tiles < 256 and tiles * sk <= 768)) \
                         and (cfg, sk) not in out:
@@ -100,8 +98,6 @@ def candidates(m, n, k, mode, keep=6):
             tiles = -(-m // bm) * -(-n // bn)
             if bm > 2 * m and cfg != 33 and cfg != 36 and cfg != 39:
                 continue  # x tile far taller than M
-            if cfg in (36, 38, 39) and G._pp_valid(cfg, n, k, mode, 0):
-                out.append((cfg, 0))  # stream-K
             for sk in (1, 2, 4, 8):
                 if G._pp_valid(cfg, n, k, mode, sk) and (sk == 1 or (tiles < 256 and tiles * sk <= 1024)) \
                         and (cfg, sk) not in out:
@@ -288,8 +284,8 @@ def tune_fp8(args, merged_unused):
                 for c in range(4):
                     bm, bn = G_F8[c]
                     tiles = -(-m // bm) * (n // bn)
-                    for sk in (0, 1, 2, 4):  # 0: stream-K
-                        if (n % bn == 0) and (sk == 0 or (k // 128) % sk == 0) and (sk <= 1 or tiles * sk <= 768):
+                    for sk in (1, 2, 4):
+                        if (n % bn == 0) and (k // 128) % sk == 0 and (sk == 1 or tiles * sk <= 768):
                             lgc.append((c, sk))
 
             def lib(i):

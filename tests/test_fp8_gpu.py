@@ -161,12 +161,10 @@ def test_fp8_model_tracks_bf16_and_engine_valid():
 
 @pytest.mark.parametrize("cfg", [0, 1, 2, 3])
 @pytest.mark.parametrize("m,n,k,swiglu,splitk", [(300, 2048, 2048, False, 1), (257, 1024, 4096, True, 1),
-                                                 (130, 2052, 1024, False, 2), (77, 512, 2048, True, 4),
-                                                 (700, 2048, 2048, False, 0), (300, 1024, 1024, True, 0)])
+                                                 (130, 2052, 1024, False, 2), (77, 512, 2048, True, 4)])
 def test_qgemm_lg(cfg, m, n, k, swiglu, splitk):
     """gemm_lg.hip's fp8 configs (ring schedule, one v_mfma_scale_f32_16x16x128_f8f6f4 k-step per 128-B stage) against
-    the fp32 reference: partial M and N tiles (N % 4 only, plain), SwiGLU, split-K and stream-K (splitk 0; tickets
-    left at zero: 3 calls)."""
+    the fp32 reference: partial M and N tiles (N % 4 only, plain), SwiGLU, split-K (tickets left at zero: 3 calls)."""
     from chronos.ops import reference as ref
 
     g = torch.Generator(device=DEV).manual_seed(cfg * 31 + m + n + k)

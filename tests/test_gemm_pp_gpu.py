@@ -120,37 +120,3 @@ def test_decode_shapes_vs_library():
         lib = x @ w.t()
         err = (y.float() - lib.float()).abs().max().item()
         assert err <= 2e-2 * lib.float().abs().max().item()
-
-
-@pytest.mark.parametrize("cfg", [20, 29, 30, 19, 38, 39])
-@pytest.mark.parametrize("m,n,k", [(300, 512, 64 * 20), (1024, 2048, 4096), (2048, 4096, 128), (77, 1536, 64 * 7)])
-def test_stream_k(cfg, m, n, k):
-    """splitk = 0: stream-K (one workgroup per CU walks an even share of tiles x K units; partial passes hand off
-    through fp32 slabs and a per-tile ticket).  Covers tiles split into many passes (few units per workgroup), whole
-    tiles plus boundary passes, and several whole tiles per workgroup; tickets must be left at zero (3 calls)."""
-    g = torch.Generator(device=DEV).manual_seed(13 * cfg + m + k)
-    x = _rand((m, k), g)
-    w = _rand((n, k), g, 0.5, 0.05)
-    ref = x.float() @ w.float().t()
-    for _ in range(3):
-        y, _ = _pp(x, w, 0, cfg, 0)
-        _check(y, ref)
-
-
-@pytest.mark.parametrize("cfg", [20, 30, 38])
-def test_stream_k_epilogues(cfg):
-    """Stream-K with the SwiGLU and residual + RMSNorm-partials epilogues (the last arriver of a split tile runs them)."""
-    g = torch.Generator(device=DEV).manual_seed(5 + cfg)
-    m, f, k = 520, 512, 64 * 9
-    x = _rand((m, k), g)
-    w = _rand((2 * f, k), g, 0.3)
-    hv = x.float() @ w.float().t()
-    y, _ = _pp(x, w, 1, cfg, 0)
-    _check(y, torch.nn.functional.silu(hv[:, :f]) * hv[:, f:], 3e-2)
-    n = 1024
-    w2 = _rand((n, k), g, 0.2)
-    r = _rand((m, n), g, 4.0)
-    s, part = _pp(x, w2, 2, cfg, 0, r)
-    ref = (x.float() @ w2.float().t()).to(torch.bfloat16).float() + r.float()
-    _check(s, ref)
-    assert torch.allclose(part.sum(1), (s.float() ** 2).sum(1), rtol=1e-4, atol=1e-3)
