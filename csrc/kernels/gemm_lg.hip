@@ -1,36 +1,33 @@
-// gemm_lg.hip — the large-M projection GEMM (SURVEY.md §2.3 K3 / K7 / K8+K9 / K10 / K11 at M >= 256):
-// y[M, N] = x[M, K] · W[N, K]^T, bf16 in, fp32 accumulate, the Llama decoder's epilogues fused in (same PPArgs and
-// epilogue contract as gemm_pp.hip, which it replaces at large M).
+// gemm_lg.hip — the software-pipelined projection GEMM family (SURVEY.md §2.3 K3 / K7 / K8+K9 / K10 / K11):
+// y[M, N] = x[M, K] · W[N, K]^T, bf16 (or W8A8 e4m3fn) in, fp32 accumulate, the Llama decoder's epilogues fused in
+// (same PPArgs and epilogue contract as gemm_pp.hip).  One kernel template, three tile regimes routed per shape by
+// ops/gemm_plan.json: 256-row tiles for M >= 512 (the 1024-row decode step), 64-W-row tiles with 64-256-row x panels
+// for M = 48-512, 32-row x tiles for M <= 48; and fp8 configs of the ring schedule for W8A8.
 //
-// Structure: ONE wave per SIMD and a software-pipelined main loop with exactly one workgroup barrier per K stage.
-//
-//   * 256-thread workgroup = 4 waves in a 2 x 2 grid; wave (wi, wj) owns W rows [wi*WN/2, +WN/2) and x rows
-//     [wj*XM/2, +XM/2) of the WN x XM output tile — 128 x 128 per wave for the 256 x 256 tile: 64 accumulators of
-//     v_mfma_f32_16x16x32_bf16 (256 registers; the unified VGPR/AGPR file holds them next to two fragment sets);
+//   * workgroup = 2 x NWX waves (NWX = 2: one wave per SIMD, 4: two); wave (wi, wj) owns W rows [wi*WN/2, +WN/2) and
+//     x rows [wj*XM/NWX, +XM/NWX) of the WN x XM output tile (the production 256 x 256 tile: 8 waves, 128 x 64 each);
 //   * swapped product D = W · x^T: a lane's accumulator holds 4 CONSECUTIVE output columns of one output row, so the
-//     row epilogues (residual, RMSNorm partials, folded-norm scale, SwiGLU pairs) need no cross-lane traffic beyond the
-//     4 lanes of a row;
-//   * operands reach LDS only through LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave-instruction) into an ST-deep
-//     ring of BK = RB/2 deep stages; the 16-B chunk swizzle is applied on the per-lane SOURCE address and undone on the
-//     ds_read_b128 fragment read (cdna_hip_programming.md §5.4 rule 21, T2), conflict-free for the 16x16x32 maps;
-//   * stage t, with the fragments of stage t already in registers (set t & 1):
+//     row epilogues (residual, RMSNorm partials, folded-norm scale, SwiGLU pairs, fp8 scales) need no cross-lane
+//     traffic beyond the 4 lanes of a row;
+//   * operands reach LDS only through LDS-DMA (buffer_load_dwordx4 ... lds through one buffer descriptor per operand:
+//     32-bit per-lane offsets, rows past the end read as zeros by the range check); the 16-B chunk swizzle is applied on
+//     the per-lane SOURCE address and undone on the ds_read_b128 fragment read (cdna_hip_programming.md §5.4 rule 21,
+//     T2), conflict-free for the 16x16x32 maps;
+//   * ring schedule (ST >= 3), stage t with its fragments already in registers (set t & 1):
 //         part 1: DMA issue of stage t+ST-1 (into the buffer every wave finished reading before the previous
 //                 barrier)  ||  the first half of the stage's MFMAs
 //         s_waitcnt vmcnt(n): this wave's DMA of stage t+1 has landed, stages t+2 .. t+ST-1 stay in flight
 //         s_barrier          : every wave's DMA of stage t+1 has landed -> visible to every wave
 //         part 2: ds_read of stage t+1's fragments into the other register set  ||  the second half of the MFMAs
-//     so the MFMA pipe never waits for LDS after a barrier (the next stage's fragments were read under this stage's
-//     MFMAs), the DMA of a stage has ~1.5 stages of MFMA time to land, and the only sync point per stage is one raw
-//     s_barrier (never __syncthreads, whose vmcnt(0) would drain the ring).  The instruction interleave inside each
-//     part is fixed with __builtin_amdgcn_sched_group_barrier (T19): 1 DMA per MFMA group in part 1, 1 ds_read per
-//     MFMA group in part 2;
+//     slab schedule (ST == 2, 64-deep slabs in two buffers): fragments pipelined per 32-deep k-step, one barrier per
+//     slab (below).  The only sync point is a raw s_barrier (never __syncthreads, whose vmcnt(0) would drain the ring);
+//     the interleave inside each part is fixed with __builtin_amdgcn_sched_group_barrier (T19);
 //   * split-K (shapes whose tile grid under-fills 256 CUs): fp32 slabs, an agent release / acquire ticket, the last
 //     arriver sums the slabs in slice order and runs the epilogue (cdna_hip_programming.md §5 "In-launch split-K");
 //   * XCD-aware task order (xcd_remap + M-tile grouping as in gemm_pp.hip): the tiles an XCD runs together share x
 //     rows and W rows in its L2.  Correctness never depends on placement.
 //
-// Replaces, at M >= 256, what round 3 left on hipBLASLt (VERDICT r3 "what's missing" 1: a barrier-driven ping-pong
-// loop with two 32-MFMA intervals per stage waited 34 % of its wave cycles).
+// What bounds the large-M configs against hipBLASLt (ablations, PMC, microbenchmarks): profiles/r4_studies.md.
 #include "chronos_hip.h"
 #include "chronos_gemm.h"
 
