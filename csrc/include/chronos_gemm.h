@@ -17,6 +17,7 @@ struct PPArgs {
     int M, N, K, F, nparts_in, splitk, kts;
     float eps;
     int gm;      // tile order: M-tiles per group (0 = every M-tile of a W panel consecutive); knob pp_gm
+    int handoff;       // gemm_lg split-K slab hand-off (knob lg_handoff): -1 auto, 0 fences, 1 write-through
     const float* xsc;  // gemm_lg F8 (W8A8 e4m3fn bytes in x / w): per-token scales [M]
     const float* wsc;  // ... and per-output-channel scales [N]
     int ablate;  // timing-only diagnostics (knob pp_ablate): 1 skip loop DMA, 2 skip LDS reads, 4 skip MFMA, 8 nt weights, 16/32 alias every W/x tile onto tile 0

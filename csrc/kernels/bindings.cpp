@@ -526,6 +526,7 @@ std::tuple<Tensor, Tensor> gemm_pp(const Tensor& x, const Tensor& w, int64_t mod
     a.eps = (float)eps;
     a.ablate = chronos::knob("pp_ablate", 0);
     a.gm = chronos::knob("pp_gm", 8);  // +7-9 % at M = 16384 (profiles/r3_gemm_tile_order_m16384.jsonl)
+    a.handoff = chronos::knob("lg_handoff", -1);
     Tensor y = at::empty({M, mode == 1 ? N / 2 : N}, x.options());
     a.y = bfm(y);
     Tensor part_out;
@@ -697,6 +698,7 @@ Tensor qgemm_lg(const Tensor& xq, const Tensor& xs, const Tensor& wq, const Tens
     a.splitk = (int)splitk;
     a.kts = (int)(K / 128 / splitk);
     a.gm = chronos::knob("pp_gm", 8);
+    a.handoff = chronos::knob("lg_handoff", -1);
     Tensor y = at::empty({M, swiglu ? N / 2 : N}, xq.options().dtype(at::kBFloat16));
     a.y = bfm(y);
     const int64_t tiles = ((M + BM - 1) / BM) * (swiglu ? (N / 2) / (BN / 2) : (N + BN - 1) / BN);

@@ -508,22 +508,31 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
 
     // ---- split-K: fp32 slab in register order, ticket, the last arriver sums every slab in slice order
     if (S > 1) {
+        // slab hand-off: plain stores + agent release / acquire fences (each a write-back / invalidate of the XCD's
+        // L2), or write-through stores + agent-scope loads with no fence (gemm_skinny.hip's form).  Write-through
+        // wins on the 8-16 KB slabs of the 32/64-row tiles (O M = 128 cfg39 split-K 2: 17.5 vs 20.1 us) and loses
+        // from 32 KB up (256 KB: 15-20 % slower; profiles/r4_gemm_lg_handoff_small_ab.jsonl,
+        // r4_gemm_lg_streamk_handoff_ab.jsonl).  a.handoff: knob lg_handoff (-1 auto, 0 fences, 1 write-through)
+        const bool wt = a.handoff < 0 ? WN * XM * 4 <= 16384 : a.handoff != 0;
         float* slab = a.ws + (int64_t)task * (WN * XM);
 #pragma unroll
         for (int s = 0; s < NT; ++s)
 #pragma unroll
-            for (int u = 0; u < MT; ++u)
-                *reinterpret_cast<f32x4*>(slab + (((wave * NT + s) * MT + u) * 64 + lane) * 4) = acc[s][u];
+            for (int u = 0; u < MT; ++u) {
+                float* p = slab + (((wave * NT + s) * MT + u) * 64 + lane) * 4;
+                if (wt) st_wt(p, acc[s][u]);
+                else *reinterpret_cast<f32x4*>(p) = acc[s][u];
+            }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         int* flag = reinterpret_cast<int*>(smem + EXTRA);
         if (tid == 0) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            if (!wt) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             const int old = __hip_atomic_fetch_add(a.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const int last = old == S - 1;
             if (last) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                if (!wt) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __hip_atomic_store(a.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
@@ -537,7 +546,8 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
             for (int s = 0; s < NT; ++s)
 #pragma unroll
                 for (int u = 0; u < MT; ++u) {
-                    const f32x4 v = *reinterpret_cast<const f32x4*>(sl + (((wave * NT + s) * MT + u) * 64 + lane) * 4);
+                    const float* p = sl + (((wave * NT + s) * MT + u) * 64 + lane) * 4;
+                    const f32x4 v = wt ? ld_wt(p) : *reinterpret_cast<const f32x4*>(p);
                     acc[s][u] = o == 0 ? v : acc[s][u] + v;
                 }
         }

@@ -3,11 +3,11 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-O=gpurun_out/tune5
+O=gpurun_out/${OUT:-tune5}
 mkdir -p $O
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gemm_pp_gpu.py > $O/test.log 2>&1 || { tail -30 $O/test.log; exit 1; }
 tail -1 $O/test.log
-timeout -k 10 1000 python -u scripts/tune_gemm_pp.py --models 8b,70b-tp8 --ms 48,64,128,256,512 \
+timeout -k 10 1000 python -u scripts/tune_gemm_pp.py --models 8b,70b-tp8 --ms ${MS:-48,64,128,256,512} \
   --rounds 3 --merge project-chronos-distributed-behavioral-edr-ebpf-llm-_amd/ops/gemm_plan.json \
   --out-plan $O/plan.json --out-table $O/table.jsonl > $O/tune.log 2>&1 || { tail -30 $O/tune.log; exit 1; }
 tail -2 $O/tune.log

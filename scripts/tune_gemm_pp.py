@@ -48,14 +48,15 @@ def skinny_candidates(m, n, k, mode, keep=10):
 
 
 def tiny_candidates(m, n, k, mode):
-    """M < 16: the 32-row-x-tile gemm_lg configs (72-75), split-K while the tile grid under-fills the chip."""
+    """M < 16: the 32-row-x-tile gemm_lg configs (72-75), split-K up to ~8 workgroups per CU (at this M the fp32
+    partials are a few KB per task: the split buys load balance and loads in flight, not arithmetic)."""
     from chronos.ops import gemm as G
 
     out = []
     for cfg in (72, 73, 74, 75):
         tiles = -(-n // G._PP_BN[cfg])
         for sk in (1, 2, 4, 8):
-            if G._pp_valid(cfg, n, k, mode, sk) and (sk == 1 or (tiles < 256 and tiles * sk <= 1024)):
+            if G._pp_valid(cfg, n, k, mode, sk) and (sk == 1 or tiles * sk <= 2048):
                 out.append((cfg, sk))
     return out
 
