@@ -36,6 +36,7 @@ constexpr int kLGConfigs = 28;
 constexpr int kLGTinyFirst = 72, kLGTinyConfigs = 4;  // gemm_lg 72-75 (after the 40-71 timing-ablation ids)
 int gemm_lg_xm(int cfg);  // x rows per tile
 int gemm_lg_wn(int cfg);  // W rows per tile
+bool gemm_lg_ablations_built();  // the timing-only ablation ids 40-71 exist (CHRONOS_GEMM_ABLATIONS build)
 bool launch_gemm_lg(int cfg, int mode, bool normp, const PPArgs& a, hipStream_t st);
 // W8A8 fp8 configs of the same kernel (ring schedule, 128-deep stages; a.kts counts 128-deep units), own id space
 constexpr int kLGF8Configs = 4;

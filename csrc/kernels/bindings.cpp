@@ -500,7 +500,9 @@ std::tuple<Tensor, Tensor> gemm_pp(const Tensor& x, const Tensor& w, int64_t mod
     const int64_t K = x.size(-1), M = x.numel() / K, N = w.size(0);
     CHK(w.dim() == 2 && w.size(1) == K, "gemm_pp: w must be [N, K]");
     const bool lg = cfg >= chronos::kPPConfigs;  // gemm_lg.hip configs continue the id space
-    CHK((cfg >= 0 && cfg < chronos::kPPConfigs + chronos::kLGConfigs) || (cfg >= 40 && cfg < 72) ||
+    // 40-71: gemm_lg's timing-only ablations (wrong results by design), rejected unless built in
+    CHK((cfg >= 0 && cfg < chronos::kPPConfigs + chronos::kLGConfigs) ||
+            (chronos::gemm_lg_ablations_built() && cfg >= 40 && cfg < 72) ||
             (cfg >= chronos::kLGTinyFirst && cfg < chronos::kLGTinyFirst + chronos::kLGTinyConfigs), "gemm_pp: cfg");
     CHK(mode >= 0 && mode <= 2, "gemm_pp: mode");
     const int BM = lg ? chronos::gemm_lg_xm((int)cfg) : chronos::gemm_pp_bm((int)cfg);
@@ -524,7 +526,8 @@ std::tuple<Tensor, Tensor> gemm_pp(const Tensor& x, const Tensor& w, int64_t mod
     a.splitk = (int)splitk;
     a.kts = (int)(K / 64 / splitk);
     a.eps = (float)eps;
-    a.ablate = chronos::knob("pp_ablate", 0);
+    // timing-only diagnostics (wrong results by design): honoured only in a CHRONOS_GEMM_ABLATIONS build
+    a.ablate = chronos::gemm_lg_ablations_built() ? chronos::knob("pp_ablate", 0) : 0;
     a.gm = chronos::knob("pp_gm", 8);  // +7-9 % at M = 16384 (profiles/r3_gemm_tile_order_m16384.jsonl)
     a.handoff = chronos::knob("lg_handoff", -1);
     Tensor y = at::empty({M, mode == 1 ? N / 2 : N}, x.options());

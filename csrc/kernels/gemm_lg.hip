@@ -683,7 +683,9 @@ bool lg_mode(int cfg, const PPArgs& a, hipStream_t st) {
 #undef LG_CASE
         default: break;
     }
-    // timing-only ablations of configs 12 / 16 (plain mode): 40 + 8 * (cfg == 16) + ABL
+    // timing-only ablations of configs 12 / 16 (plain mode): 40 + 8 * (cfg == 16) + ABL.  Several return wrong results
+    // by design, so they exist only in a diagnostics build (CHRONOS_GEMM_ABLATIONS=1 at build time, native.py)
+#ifdef CHRONOS_GEMM_ABLATIONS
     if constexpr (MODE == kPlain && !NORMP) {
         switch (cfg) {
             case 41: lg_launch<256, 256, 64, 4, MODE, NORMP, 2, 1>(a, st); return true;
@@ -711,13 +713,22 @@ bool lg_mode(int cfg, const PPArgs& a, hipStream_t st) {
             default: break;
         }
     }
+#endif
     return false;
 }
 
 }  // namespace
 
+bool gemm_lg_ablations_built() {
+#ifdef CHRONOS_GEMM_ABLATIONS
+    return true;
+#else
+    return false;
+#endif
+}
+
 int gemm_lg_xm(int cfg) {
-    if (cfg >= 40 && cfg < 72) return 256;  // ablation ids
+    if (gemm_lg_ablations_built() && cfg >= 40 && cfg < 72) return 256;  // ablation ids
     switch (cfg) {
 #define LG_XM(ID, WN_, XM_, RB_, ST_, NWX_, ...) case ID: return XM_;
         LG_CONFIGS(LG_XM)
@@ -726,7 +737,7 @@ int gemm_lg_xm(int cfg) {
     }
 }
 int gemm_lg_wn(int cfg) {
-    if (cfg >= 40 && cfg < 72) return 256;
+    if (gemm_lg_ablations_built() && cfg >= 40 && cfg < 72) return 256;
     switch (cfg) {
 #define LG_WN(ID, WN_, XM_, RB_, ST_, NWX_, ...) case ID: return WN_;
         LG_CONFIGS(LG_WN)

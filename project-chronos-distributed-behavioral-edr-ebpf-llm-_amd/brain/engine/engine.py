@@ -2,9 +2,17 @@
 
 Replaces what Ollama + llama.cpp did for the reference:
 
-* **admission**: a request gets a decode *slot* and ALL the KV blocks it can ever need (prompt + num_predict) up
-  front, so a running sequence never stalls or gets preempted mid-verdict; KV is sized from the HBM budget
-  (288 GB per MI355X — 1-2 M tokens for 8B, SURVEY.md App. C);
+* **admission**: a request gets a decode *slot* and the KV blocks of its prompt plus ``kv_lookahead`` generated
+  tokens (``kv_alloc="lazy"``, the default; ``"full"`` reserves prompt + num_predict up front as rounds 1-4 did).
+  KV is sized from the HBM budget (288 GB per MI355X — 1-2 M tokens for 8B, SURVEY.md App. C);
+* **KV growth and preemption** (SURVEY.md §7.2 step 6): before every launch that writes generated-token KV (decode
+  burst, mixed step, jump-forward) each running sequence's blocks are grown to cover the positions that launch can
+  write (a host-side upper bound, ``Request.pos_hi``).  When the pool runs dry the NEWEST running sequences are
+  preempted by recompute: their exact device state (generated ids, grammar state) is read back, their computed full
+  blocks are published to the prefix cache, their blocks and slot are freed, and they go back to the FRONT of the
+  queue with the generated ids appended to the prompt, the grammar resuming from the saved state.  A resumed greedy
+  request produces the tokens an uninterrupted run would have (the re-prefill computes the pending token's logits
+  exactly as the decode step would have);
 * **prefill**: waiting prompts are packed into one flattened token stream (chunked to ``max_prefill_tokens``, so a
   128k-token chain context prefills in pieces that attend to the paged prefix);
 * **decode**: all slots advance together; the step (32 layers + LM head + the constrained sampler, which also
@@ -79,6 +87,11 @@ class EngineConfig:
     prefill_nqt: int = 8           # 8 = flash prefill kernel (128 query rows / workgroup); 1-2 = split-K kernel
     async_harvest: bool = False    # harvest burst k while burst k+1 runs (hides host work, delays compaction)
     request_timeout_s: float = 0.0  # >0: a request not finished this long after submit is cancelled (reason "timeout")
+    # KV reservation: "lazy" = prompt + kv_lookahead tokens at admission, grown per launch, recompute preemption of the
+    # newest sequences when the pool runs dry; "full" = prompt + num_predict at admission (never preempts)
+    kv_alloc: str = "lazy"
+    kv_lookahead: int = 64         # generated-token headroom allocated per growth (amortises the block-table updates)
+    kv_watermark: float = 0.01     # lazy admission leaves this fraction of the pool free for the running rows' growth
     tp_overlap: bool = True        # TP prefill: two micro-batches, each one's RCCL all-reduces overlap the other's compute
     tp_overlap_min_tokens: int = 1024
     tp_sequence_parallel: bool = False  # TP prefill: reduce-scatter / all-gather around the norms instead of all-reduce
@@ -140,6 +153,17 @@ class Request:
     t_admit: float = 0.0
     t_first: float = 0.0
     t_done: float = 0.0
+    # KV growth / preemption (lazy reservation): upper bound of the next KV position a queued launch may write, ids
+    # generated before a preemption (the re-prefilled prompt carries them), prompt length as submitted
+    pos_hi: int = 0
+    resume_out: list = field(default_factory=list)
+    orig_plen: int = -1
+    preemptions: int = 0
+
+    @property
+    def kv_cap(self) -> int:
+        """KV slots this request can ever write: prompt + num_predict (the last sampled token is never written)."""
+        return len(self.prompt_ids) + self.num_predict
 
     @property
     def latency(self) -> float:
@@ -361,6 +385,9 @@ class Engine:
             with trace.range("decode_burst"):
                 snap = self._decode_burst()
             reaped = reaped + self._flush_deferred()  # while the burst runs
+            if snap is None:  # every row was preempted for KV: they re-prefill next step
+                self._pending = None
+                return reaped
             t2 = pc()
             ph["decode_launch"] += t2 - t1
             if not self._async:
@@ -497,9 +524,15 @@ class Engine:
                     if not self._check_length(req):
                         self.waiting.popleft()
                         continue
-                nblk = self.blocks.blocks_for(len(req.prompt_ids) + req.num_predict)
+                nblk, wm = self._admit_blocks(req)
+                if nblk > self.blocks.num_blocks - 1:  # could never fit, even alone: an error, not a stalled queue
+                    self.waiting.popleft()
+                    req.error = (f"prompt of {len(req.prompt_ids)} tokens needs {nblk} KV blocks, the cache holds "
+                                 f"{self.blocks.num_blocks - 1}")
+                    self._finish(req, "error")
+                    continue
                 shared = self.blocks.lookup(req.prompt_ids)  # cached prefix blocks (already referenced)
-                if not self.blocks.can_alloc(nblk - len(shared)):
+                if not self.blocks.can_alloc(nblk - len(shared) + (wm if self.running else 0)):
                     self.blocks.release(shared)
                     break
                 self.waiting.popleft()
@@ -525,6 +558,127 @@ class Engine:
                 self.prefilling.append(req)
                 budget -= len(req.prompt_ids) - req.prefilled
         # (the slots' block-table rows are published when their prompts finish: _init_slots)
+
+    def _admit_blocks(self, req: Request) -> tuple[int, int]:
+        """(KV blocks a request takes at admission, free blocks lazy admission leaves for the running rows)."""
+        if self.cfg.kv_alloc == "full":
+            return self.blocks.blocks_for(req.kv_cap), 0
+        toks = min(req.kv_cap, len(req.prompt_ids) + self.cfg.kv_lookahead)
+        return self.blocks.blocks_for(toks), int(self.cfg.kv_watermark * self.blocks.num_blocks)
+
+    # ---- KV growth and recompute preemption (kv_alloc="lazy") -------------------------------------------------------
+    def _ensure_kv(self, extra: list) -> None:
+        """Grow running sequences' blocks so the launch about to be queued can write its KV.  ``extra``: (request,
+        KV slots (positions + 1) that launch may write for it).  Oldest requests are served first; when the pool is
+        short, the newest running requests are preempted (recompute) until it is not.  Updates the slot block
+        tables of every grown row in one device write."""
+        bs = self.blocks.block_size
+        grown = []
+        for r, need in sorted(extra, key=lambda e: e[0].rid):
+            if self.running.get(r.slot) is not r:
+                continue  # preempted as a victim of an older request's growth
+            need = min(r.kv_cap, need)
+            have = len(r.blocks) * bs
+            if need <= have:
+                continue
+            want = self.blocks.blocks_for(need) - len(r.blocks)
+            while not self.blocks.can_alloc(want):
+                victim = max((q for q in self.running.values()), key=lambda q: q.rid)
+                self._preempt(victim)
+                if victim is r:
+                    break
+            if self.running.get(r.slot) is not r:
+                continue
+            more = self.blocks.blocks_for(min(r.kv_cap, need + self.cfg.kv_lookahead)) - len(r.blocks)
+            take = max(want, min(more, self.blocks.free))
+            old = len(r.blocks)
+            r.blocks += self.blocks.alloc(take)
+            grown.append((r, old))
+            self.stats["kv_grow_blocks"] += take
+        if grown:
+            rows, cols, vals = [], [], []
+            for r, old in grown:
+                for j in range(old, len(r.blocks)):
+                    rows.append(r.slot)
+                    cols.append(j)
+                    vals.append(r.blocks[j])
+            dv = lambda t: h2d(t, self.device)  # noqa: E731
+            self.s_bt[dv(torch.tensor(rows, dtype=torch.int64)), dv(torch.tensor(cols, dtype=torch.int64))] = dv(
+                torch.tensor(vals, dtype=torch.int32))
+
+    def _preempt(self, r: Request) -> None:
+        """Recompute preemption of a running request: read its exact device state (a sync — preemption is rare),
+        publish its computed full blocks to the prefix cache, free its blocks and slot, and queue it at the front
+        with the generated ids appended to its prompt and its grammar resuming from the saved state.  A request whose
+        verdict already closed on device is finished instead (nothing to recompute)."""
+        s = r.slot
+        st = int(self.s_state[s].item())
+        n = min(int(self.s_nout[s].item()), self.cfg.max_out)
+        out = self.s_out[s, :n].tolist() if n else []
+        del self.running[s]
+        r.slot = -1
+        self._free_slots([s])
+        if st == DONE:  # finished on device, not harvested yet: complete it now
+            stop = bool(out) and out[-1] in self.tok.stop_ids
+            r.out_ids = r.resume_out + (out[:-1] if stop else out)
+            r.t_done = time.perf_counter()
+            self.blocks.release(r.blocks)
+            r.blocks = []
+            self.stats["completed"] += 1
+            self._deferred.append((r, "stop" if stop else "length"))
+            return
+        on_tok = r.meta.get("on_tokens")
+        if on_tok is not None:  # stream what this run produced before it is folded into the prompt
+            e = r.meta.get("emitted", 0)
+            if n > e:
+                try:
+                    on_tok(out[e:n])
+                except Exception:
+                    log.exception("stream callback failed")
+            r.meta["emitted"] = 0
+        plen = len(r.prompt_ids)
+        if r.orig_plen < 0:
+            r.orig_plen = plen
+        ctx = r.prompt_ids + out
+        # KV exists for positions < plen + n - 1 (the last sampled token is pending): publish those full blocks, so
+        # the re-admission's prefix lookup finds them unless they are evicted first
+        self.blocks.register(ctx[:plen + n - 1] if n else ctx, r.blocks)
+        self.blocks.release(r.blocks)
+        r.blocks = []
+        r.prompt_ids = ctx
+        r.resume_out = r.resume_out + out
+        r.num_predict -= n
+        r.start_state = -2 - st if st <= -2 else st
+        r.prefilled = 0
+        r.preemptions += 1
+        r.meta.pop("jump_seq", None)
+        r.meta["preempt_seq"] = self._snap_seq  # snapshots queued so far hold this run's rows, not the next one's
+        self.stats["preemptions"] += 1
+        with self._lock:
+            self.waiting.appendleft(r)
+
+    def _free_slots(self, slots: list) -> None:
+        """Return slots to the free list and park their device state (empty, scratch block table)."""
+        self.free_slots.extend(slots)
+        self.free_slots.sort(reverse=True)
+        idx = h2d(torch.tensor(slots, dtype=torch.int64), self.device)
+        self.s_state.index_fill_(0, idx, -1)
+        self.s_bt.index_fill_(0, idx, 0)
+        self.s_pos.index_fill_(0, idx, 0)
+        self.s_ctx.index_fill_(0, idx, 1)
+
+    def _grow_for(self, k: int) -> None:
+        """Lazy KV: every running row may write k more KV positions in the launch about to be queued (a decode burst
+        of k steps, or a mixed step's one): grow whoever needs it, then advance the bound."""
+        if self.cfg.kv_alloc != "lazy" or not self.running:
+            return
+        bs = self.blocks.block_size
+        extra = [(r, r.pos_hi + k) for r in self.running.values()
+                 if r.pos_hi + k > len(r.blocks) * bs and len(r.blocks) * bs < r.kv_cap]
+        if extra:
+            self._ensure_kv(extra)
+        for r in self.running.values():
+            r.pos_hi += k
 
     def _copy_partial_blocks(self) -> None:
         """Batched copy of the partial-prefix source blocks into their new owners (every layer's K and V, whole
@@ -561,6 +715,7 @@ class Engine:
             if req.prefilled == len(req.prompt_ids):
                 done_rows.append(i)
                 done_reqs.append(req)
+                req.pos_hi = len(req.prompt_ids)  # the first sampled token is written there by the next decode step
                 self.blocks.register(req.prompt_ids, req.blocks)
         self.stats["prefill_tokens"] += sum(len(c) for c in chunks)
         self.stats["prefill_steps"] += 1
@@ -652,6 +807,10 @@ class Engine:
         after step i+1 was queued, so the host never waits for the GPU it is about to feed."""
         if self._copies:
             self._copy_partial_blocks()
+        self._grow_for(1)  # (may preempt: the bucket below is sized after it)
+        if not self.running:
+            self._prefill_step()
+            return []
         n = min(self._decode_rows(), self.cfg.max_slots)
         budget = min(self._ramp, max(self.cfg.mixed_prefill_tokens, self.cfg.mixed_ratio * n))
         self._ramp = min(4 * self._ramp, self._chunk)
@@ -733,9 +892,12 @@ class Engine:
             return t
         return k
 
-    def _decode_burst(self) -> _Snapshot:
+    def _decode_burst(self) -> Optional[_Snapshot]:
+        k = self._burst_len(min(self._decode_rows(), self.cfg.max_slots))
+        self._grow_for(k)  # (may preempt: the bucket is sized after it)
+        if not self.running:
+            return None
         n = min(self._decode_rows(), self.cfg.max_slots)
-        k = self._burst_len(n)
         ns = self._nsplit(n, self._ctx_class())
         if self.device.type == "cuda" and self.cfg.use_graphs:
             g = self._graphs.get((n, ns, k))
@@ -805,7 +967,10 @@ class Engine:
             snap.event.synchronize()
             self.phase_s["harvest_gpu_wait"] += time.perf_counter() - t
         # (snapshot slot, request) for requests still running as the same object (identity, not slot number)
-        live = [(s, r) for s, r in snap.owners.items() if self.running.get(r.slot) is r]
+        # (a request preempted after this snapshot was queued may be running again in another slot: its row here
+        # belongs to the run before the preemption)
+        live = [(s, r) for s, r in snap.owners.items()
+                if self.running.get(r.slot) is r and r.meta.get("preempt_seq", -1) < snap.seq]
         if not live:
             return []
         st = snap.state[:snap.n].tolist()
@@ -820,6 +985,9 @@ class Engine:
             ended = self._jump(parked, st, nout, outs)
             self.phase_s["jump"] += time.perf_counter() - t
         finished += [(s, r) for s, r in parked if s in ended]
+        # (a jump's KV growth may have preempted some of these rows: they are queued again, not finished)
+        finished = [(s, r) for s, r in finished if self.running.get(r.slot) is r]
+        live = [(s, r) for s, r in live if self.running.get(r.slot) is r]
         streaming = [(s, r) for s, r in live if r.meta.get("on_tokens")]
         if not finished and not streaming:
             return []
@@ -843,7 +1011,7 @@ class Engine:
             k = int(nout[s])
             ids = ended[s] if s in ended else outs[s, :min(k, self.cfg.max_out)].tolist()
             stop = bool(ids) and ids[-1] in self.tok.stop_ids
-            r.out_ids = ids[:-1] if stop else ids
+            r.out_ids = r.resume_out + (ids[:-1] if stop else ids)
             r.t_done = now
             del self.running[r.slot]
             self.blocks.release(r.blocks)
@@ -895,7 +1063,7 @@ class Engine:
                 self.stats["jump_refused"] += 1
                 continue
             ids = outs[s, :n0].tolist() + list(run)
-            r.meta.setdefault("jump_spans", []).append((n0, k))
+            r.meta.setdefault("jump_spans", []).append((len(r.resume_out) + n0, k))
             r.meta["jump_seq"] = self._snap_seq  # every snapshot queued so far predates this jump
             self.stats["jumps"] += 1
             self.stats["jump_tokens"] += k
@@ -907,6 +1075,10 @@ class Engine:
         if unpark:
             self.s_state[dv(torch.tensor([u[0] for u in unpark], dtype=torch.int64))] = dv(
                 torch.tensor([u[1] for u in unpark], dtype=torch.int32))
+        if rows and self.cfg.kv_alloc == "lazy":
+            # the forward writes positions pos0 .. pos0 + k: grow (preempting the newest rows if the pool is short)
+            self._ensure_kv([(r, len(r.prompt_ids) + n0 + k) for r, _, _, n0, k in rows])
+            rows = [x for x in rows if self.running.get(x[0].slot) is x[0]]
         if not rows:
             return ended
         pos0 = [len(r.prompt_ids) + n0 - 1 for r, _, _, n0, _ in rows]
@@ -927,6 +1099,8 @@ class Engine:
         self.s_pos[sl] = i32([p + k for p, (*_, k) in zip(pos0, rows)])
         self.s_ctx[sl] = i32([p + k + 1 for p, (*_, k) in zip(pos0, rows)])
         self.s_state[sl] = i32([end for _, _, end, _, _ in rows])
+        for p, (r, *_, k) in zip(pos0, rows):
+            r.pos_hi = p + k
         self.s_row.fill_(-1)
         self.s_row[sl] = i32(list(range(len(rows))))
         ops.constrained_sample(logits, self.s_row, self.bank.next, self.bank.dist, DONE, self.s_state, self.s_rem,
@@ -969,6 +1143,10 @@ class Engine:
         self.stats["compactions"] += 1
 
     def _finish(self, req: Request, reason: str, timed: bool = True) -> None:
+        if req.orig_plen >= 0:  # preempted at least once: the prompt carried the generated ids while it re-prefilled
+            req.prompt_ids = req.prompt_ids[:req.orig_plen]
+            if not req.out_ids and req.resume_out:
+                req.out_ids = list(req.resume_out)
         req.done_reason = reason
         if timed or not req.t_done:
             req.t_done = time.perf_counter()

@@ -182,6 +182,8 @@ def hip_flags() -> tuple[list[str], list[str]]:
         "-Wno-unused-command-line-argument",
         f"-I{os.path.join(CSRC, 'include')}",
     ] + [f"-I{i}" for i in incs] + [f"-I{sysconfig.get_paths()['include']}"]
+    if os.environ.get("CHRONOS_GEMM_ABLATIONS") == "1":  # diagnostics build: gemm_lg's timing-only ablation ids
+        cflags.append("-DCHRONOS_GEMM_ABLATIONS")
     ldflags = [f"-L{libdir}", f"-Wl,-rpath,{libdir}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu",
                "-ltorch_hip", "-ltorch_python", "-lamdhip64"]
     return cflags, ldflags

@@ -65,12 +65,14 @@ def _plan_file() -> dict:
     if _plan_table is None:
         import json
 
-        path = os.environ.get("CHRONOS_GEMM_PLAN") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
-                                                                   "gemm_plan.json")
+        override = os.environ.get("CHRONOS_GEMM_PLAN")
+        path = override or os.path.join(os.path.dirname(os.path.abspath(__file__)), "gemm_plan.json")
         try:
             with open(path) as fh:
                 raw = json.load(fh)
         except FileNotFoundError:
+            if override:  # an explicit A/B override that does not exist must not silently measure the library
+                raise FileNotFoundError(f"CHRONOS_GEMM_PLAN={override!r}: no such plan file") from None
             raw = {}
         key = lambda k: tuple(int(v) for v in k.split(","))  # noqa: E731
         _plan_table = {key(k): rows for k, rows in raw.get("plans", {}).items()}

@@ -15,9 +15,11 @@ while no replica is serving) with the dead / restarting replicas and the restart
 
 Respawns are bounded: a worker that dies before reporting ready (OOM at model build, a GPU that fails to initialise)
 is a start-up failure; consecutive ones are respawned after an exponential delay (``respawn_base_s`` doubling, capped
-at ``respawn_cap_s``), and after ``max_start_failures`` in a row the replica is marked failed and never respawned
-(``failed_replicas`` in ``/healthz``) instead of initialising a GPU every poll forever.  A death after ready resets
-the count (the replica had been serving).
+at ``respawn_cap_s``).  After ``max_start_failures`` in a row the replica is marked failed (``failed_replicas`` in
+``/healthz``) and from then on retried only every ``failed_retry_s`` (default: ``respawn_cap_s``), so a transient
+cause (GPU memory not yet released, a driver hiccup) does not remove it for the router's life while a persistent one
+costs one GPU initialisation per interval, not one per poll.  ``reset_replica(r)`` retries a failed replica at once.
+A replica that reports ready leaves the failed state; a death after ready resets the count (it had been serving).
 """
 from __future__ import annotations
 
@@ -33,8 +35,9 @@ from types import SimpleNamespace
 from typing import AsyncIterator, Optional
 
 
-def _worker(rank: int, cfg_dict: dict, req_q, res_q, device: str) -> None:
-    if os.environ.get("CHRONOS_FAULT_START_RANK") == str(rank):  # fault injection (tests): die before ready
+def _worker(rank: int, cfg_dict: dict, req_q, res_q, device: str, fail_start: bool = False) -> None:
+    if fail_start:  # fault injection, set only through DPRouter(fault_start_ranks=...): die before ready
+        print(f"[chronos router] replica {rank}: injected start-up fault (fault_start_ranks)", flush=True)
         raise SystemExit(7)
     import torch
 
@@ -96,8 +99,10 @@ def _worker(rank: int, cfg_dict: dict, req_q, res_q, device: str) -> None:
 class DPRouter:
     def __init__(self, cfg, replicas: int, device: str | None = None, start_timeout: float = 900.0,
                  respawn: bool = True, poll_s: float = 0.1, respawn_base_s: float = 1.0, respawn_cap_s: float = 60.0,
-                 max_start_failures: int = 5):
+                 max_start_failures: int = 5, failed_retry_s: Optional[float] = None,
+                 fault_start_ranks: tuple = ()):
         self.n = replicas
+        self._fault_start = set(fault_start_ranks)  # tests: these ranks' workers die before ready
         self._dev = device or ("cuda" if str(cfg.device).startswith("cuda") else "cpu")
         self._ctx = mp.get_context("spawn")
         self._cfgd = asdict(cfg)
@@ -129,6 +134,7 @@ class DPRouter:
         self._respawn_at: list = [None] * replicas
         self.respawn_base_s, self.respawn_cap_s = respawn_base_s, respawn_cap_s
         self.max_start_failures = max_start_failures
+        self.failed_retry_s = respawn_cap_s if failed_retry_s is None else failed_retry_s
         self.failed_requests = 0
         self.respawn = respawn
         self._closing = False
@@ -144,7 +150,8 @@ class DPRouter:
 
     def _spawn(self, r: int):
         self._ready_seen[r] = False
-        p = self._ctx.Process(target=_worker, args=(r, self._cfgd, self._reqs[r], self._res, self._dev), daemon=True)
+        p = self._ctx.Process(target=_worker, args=(r, self._cfgd, self._reqs[r], self._res, self._dev,
+                                                    r in self._fault_start), daemon=True)
         p.start()
         return p
 
@@ -159,6 +166,7 @@ class DPRouter:
                     self.alive[rid] = True
                     self._ready_seen[rid] = True
                     self.start_failures[rid] = 0
+                    self.failed[rid] = False
                 continue
             with self._lock:
                 w = self._waiters.get(rid)
@@ -207,10 +215,19 @@ class DPRouter:
                 if self.respawn and not self._closing:
                     sf = self.start_failures[r]
                     if sf >= self.max_start_failures:
-                        self.failed[r] = True  # keeps dying before ready: stop initialising a GPU every poll
+                        # keeps dying before ready: failed, retried only every failed_retry_s (never a hot loop)
+                        self.failed[r] = True
+                        delay = self.failed_retry_s
                     else:  # the first respawn after a serving replica died is immediate, start-up failures back off
                         delay = 0.0 if sf == 0 else min(self.respawn_base_s * 2 ** (sf - 1), self.respawn_cap_s)
-                        self._respawn_at[r] = time.time() + delay
+                    self._respawn_at[r] = time.time() + delay
+
+    def reset_replica(self, r: int) -> None:
+        """Admin path: retry a failed replica now (its start-up failure count starts over)."""
+        with self._lock:
+            self.start_failures[r] = 0
+            if self.failed[r] and self._respawn_at[r] is not None:
+                self._respawn_at[r] = time.time()
 
     def _dispatch(self, params, stream: bool, sink) -> tuple[int, int]:
         loop = asyncio.get_running_loop()
@@ -249,7 +266,9 @@ class DPRouter:
         if getattr(self, "_tok", None) is None:
             from ..brain.tokenizer import load_tokenizer
 
-            self._tok = load_tokenizer(None)
+            # the replicas' own tokenizer (EngineConfig.tokenizer): stop-cut contexts and streamed text must be
+            # decoded in the vocabulary the workers produced the ids in
+            self._tok = load_tokenizer(self._cfgd.get("tokenizer"))
         return self._tok
 
     async def generate(self, params):
@@ -296,6 +315,7 @@ class DPRouter:
         return bool(serving), {"status": status, "serving_replicas": serving, "dead_replicas": dead,
                                "restarting_replicas": restarting, "failed_replicas": failed,
                                "restarts": list(self.restarts), "start_failures": list(self.start_failures),
+                               "failed_retry_s": self.failed_retry_s,
                                "failed_over_requests": self.failed_requests}
 
     def info(self) -> dict:
