@@ -58,6 +58,10 @@ def parse():
     ap.add_argument("--no-partial-prefix", action="store_true",
                     help="reuse only whole cached KV blocks (no copy of a partially matching block's computed slots)")
     ap.add_argument("--async-harvest", action="store_true")
+    ap.add_argument("--cascade", action="store_true", help="shared-prefix cascade decode attention (off: measured "
+                    "slower, profiles/r5/cascade_ab.md)")
+    ap.add_argument("--kv-alloc", choices=["lazy", "full"], default="lazy",
+                    help="KV reservation at admission (lazy: prompt + lookahead, grown per launch, preemption)")
     ap.add_argument("--prefill-ramp", type=int, default=2048, help="first prefill step after idle (0 = full chunks)")
     ap.add_argument("--no-jump-forward", action="store_true", help="decode grammar-forced runs token by token")
     ap.add_argument("--jump-max-rows", type=int, default=None,
@@ -201,7 +205,8 @@ def main():
                        prefill_ramp=a.prefill_ramp, jump_forward=not a.no_jump_forward,
                        mixed_batching=not a.no_mixed,
                        **({"jump_max_rows": a.jump_max_rows} if a.jump_max_rows is not None else {}),
-                       weight_dtype=a.weights, tp_sequence_parallel=a.sequence_parallel)
+                       weight_dtype=a.weights, tp_sequence_parallel=a.sequence_parallel,
+                       cascade=a.cascade, kv_alloc=a.kv_alloc)
     # TP: the ranks of a replica submit the same chains in the same order and step the same deterministic scheduler,
     # so they stay in lockstep by construction (the serving path adds the leader broadcast of parallel/tp_engine.py)
     eng = Engine(cfg, tp=tp)

@@ -372,7 +372,8 @@ __global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
     const int32_t* __restrict__ block_table, int bt_stride, const int32_t* __restrict__ ctx_len,
     uint16_t* __restrict__ out, int nitems, int hq, int hkv, float scale_log2, float k_scale, float v_scale,
     const int32_t* __restrict__ gst, int gn, const int32_t* __restrict__ pos = nullptr,
-    const float* __restrict__ cos_sin = nullptr) {
+    const float* __restrict__ cos_sin = nullptr, const int32_t* __restrict__ casc = nullptr,
+    const uint16_t* __restrict__ opre = nullptr, const float* __restrict__ lpre = nullptr) {
     static_assert(!(RP && FP8), "fused RoPE / KV write: bf16 KV only");
     constexpr bool KLDS = KL && !FP8 && !PF;  // KL = false: K straight to VGPRs (A/B knob decode_klds)
     extern __shared__ __attribute__((aligned(1024))) unsigned char pd_smem[];
@@ -398,6 +399,21 @@ __global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
     // the first 64 block-table entries without waiting for ctx (entries past the context are never shuffled out):
     // the table load, ctx and pos all issue together instead of as a ctx -> table dependent pair
     int btv = lane < bt_stride ? bt[lane] : 0;
+
+    // cascade (shared prefix): a sequence whose first P blocks are the cascade prefix (casc[1..P]) and that has
+    // tokens past it starts its walk at token 16 P; casc_prefix_kernel already attended its rows over the prefix and
+    // left (normalised O, log2-sum-exp) for the merge after the loop.  The producer makes the same test.
+    int t_start = 0;
+    bool cmem = false;
+    if (casc != nullptr) {
+        const int P = casc[0];
+        if (P > 0 && ctx > 16 * P) {
+            const int cb = lane < P ? casc[1 + lane] : 0;
+            cmem = __all(lane >= P || btv == cb);
+        }
+        if (cmem) t_start = 16 * P;
+    }
+    const int tb = t_start & 31;  // the 32-token steps start at t_start: offset of the step grid
 
     const int nh = hq + 2 * hkv;  // RP: heads per token row of the QKV projection
     const int pnew = RP ? pos[seq] : 0;
@@ -433,7 +449,7 @@ __global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
     }
     // RP + KLDS: the new token's roped K is parked in the wave's spare LDS row (not in VGPRs) and copied into the K tile
     // of its step after that step's DMA lands (the DMA may still fetch the pre-write bytes from the cache)
-    const int u = pnew & 31;  // the new token's slot in its 32-token step (token <-> lane map: load() below)
+    const int u = (pnew - tb) & 31;  // the new token's slot in its 32-token step (token <-> lane map: load() below)
     const bool kwriter = RP && r == 4 * (u >> 3) + (u & 3);
     unsigned char* kpark = pd_smem + 4 * 8192 + (threadIdx.x >> 6) * 256;
     if constexpr (RP) {
@@ -472,9 +488,9 @@ __global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
     // 70-75 % busy on the wave's decode shape, profiles/r3s2_decode_attn_pmc.txt).
     auto load = [&](int t0, bf16x8 (&kf)[2][4], bf16x8 (&vf)[8]) {
         if (t0 < ctx) {
-            const int bi = t0 / block_size;  // page A; t0 % 32 == 0, so A and B sit in one 64-entry window
-            while (bi >= win + 64) {  // wave-uniform: next window of 64 block-table entries
-                win += 64;
+            const int bi = t0 / block_size;  // page A (B = bi + 1): both must sit in the 64-entry window
+            if (bi + 1 >= win + 64) {  // wave-uniform: the window of 64 block-table entries from page A on
+                win = bi;
                 btv = win + lane < nblk ? bt[win + lane] : 0;
             }
             const int64_t blkA = __shfl(btv, bi - win, 64);
@@ -537,7 +553,7 @@ __global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
     auto step = [&](int t0, bf16x8 (&kf)[2][4], bf16x8 (&vf)[8]) {
         if constexpr (KLDS) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's K pieces are in LDS (and V in VGPRs)
-            if (RP && t0 == (pnew & ~31) && kwriter) {
+            if (RP && t0 == pnew - u && kwriter) {
 #pragma unroll
                 for (int c = 0; c < 4; ++c) {
                     const int o = ((4 * c + h4) ^ kswz(u)) << 4;
@@ -641,8 +657,8 @@ __global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
     if constexpr (PF) {  // next step's K/V in flight while this one computes (two register sets, 1 wave/SIMD)
         bf16x8 kA[2][4], kB[2][4];
         bf16x8 vA[8], vB[8];
-        load(0, kA, vA);
-        for (int t0 = 0; t0 < ctx; t0 += 64) {
+        load(t_start, kA, vA);
+        for (int t0 = t_start; t0 < ctx; t0 += 64) {
             if (t0 + 32 < ctx) load(t0 + 32, kB, vB);
             step(t0, kA, vA);
             if (t0 + 32 >= ctx) break;
@@ -652,7 +668,7 @@ __global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
     } else {  // one register set: latency hidden by occupancy instead (3 waves/SIMD)
         bf16x8 kA[2][4];
         bf16x8 vA[8];
-        for (int t0 = 0; t0 < ctx; t0 += 32) {
+        for (int t0 = t_start; t0 < ctx; t0 += 32) {
             load(t0, kA, vA);
             step(t0, kA, vA);
         }
@@ -661,7 +677,25 @@ __global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
     float lt = lsum;
     lt += __shfl_xor(lt, 16, 64);
     lt += __shfl_xor(lt, 32, 64);
-    if (r < G) {
+    if (r < G && cmem) {
+        // merge with the prefix part: out = (o 2^(m - M) + Op l_p 2^(m_p - M)) / (l 2^(m - M) + l_p 2^(m_p - M)),
+        // M = max(m, lse_p), with the producer's Op = its O / l_p and lse_p = m_p + log2 l_p (scaled log2 units)
+        const int64_t row = (int64_t)seq * hq + h * G + r;
+        const float lp = lpre[row];
+        const float M = fmaxf(m, lp);
+        const float a = exp2f(m - M), b = exp2f(lp - M);
+        const float inv = 1.f / (lt * a + b);
+        const uint16_t* pp = opre + row * kD + 4 * h4;
+        uint16_t* op = out + row * kD + 4 * h4;
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) {
+            const u16x4 pv = *reinterpret_cast<const u16x4*>(pp + 16 * dt);
+            u16x4 ov;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) ov[i] = f2bf((o[dt][i] * a + bf2f(pv[i]) * b) * inv);
+            *reinterpret_cast<u16x4*>(op + 16 * dt) = ov;
+        }
+    } else if (r < G) {
         const float inv = lt > 0.f ? 1.f / lt : 0.f;
         uint16_t* op = out + ((int64_t)seq * hq + h * G + r) * kD + 4 * h4;
 #pragma unroll
@@ -674,28 +708,186 @@ __global__ void __launch_bounds__(256, OCC) paged_decode_kernel(
     }
 }
 
+// ------------------------------------------------------------------------------------------------------------------
+// Cascade decode attention, producer.  The wave's chains all start with the same prompt template,
+// so the leading KV blocks of every decode row are the SAME physical blocks (prefix cache).  The one-wave-per-(seq,
+// kv head) decode kernel re-reads them once per row; here each wave attends 16 query rows of ONE kv head — the G q
+// heads of 16 / G sequences — over the shared prefix tokens [0, 16 P) with the same MFMA mapping (S^T = K · Q^T, P
+// kept in registers, O^T += V^T · P^T), so the prefix K/V bytes are read once per 16 / G rows instead of once per row
+// and every MFMA row is a live query row (the decode kernel uses G of its 16).  Per member row it leaves the normalised
+// O (bf16) and lse = m + log2 l (scaled log2 units); paged_decode_kernel then walks only tokens >= 16 P and merges.
+// Membership (same test in both kernels): the sequence's first P block-table entries equal casc[1..P] and its context
+// is longer than the prefix.  casc[0] = P (0: off).  RP: q is the raw QKV projection, RoPE'd here per row.
+// ------------------------------------------------------------------------------------------------------------------
+template <bool RP>
+__global__ void __launch_bounds__(256) casc_prefix_kernel(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc, const uint16_t* __restrict__ vc,
+    const int32_t* __restrict__ casc, const int32_t* __restrict__ block_table, int bt_stride,
+    const int32_t* __restrict__ ctx_len, uint16_t* __restrict__ opre, float* __restrict__ lpre, int n, int hq,
+    int hkv, float scale_log2, const int32_t* __restrict__ gst, int gn, const int32_t* __restrict__ pos,
+    const float* __restrict__ cos_sin) {
+    constexpr int block_size = 16;
+    if (gate_closed(gst, gn)) return;
+    const int P = casc[0];
+    if (P <= 0) return;
+    const int L = block_size * P;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int h = blockIdx.y, G = hq / hkv, SPW = 16 / G;
+    const int r = lane & 15, h4 = lane >> 4;
+    const int seq = (blockIdx.x * 4 + wv) * SPW + r / G;  // this lane's query row: (seq, head)
+    const int head = h * G + r % G;
+    bool mem = seq < n;
+    if (mem) {
+        mem = ctx_len[seq] > L;
+        const int32_t* bt = block_table + (int64_t)seq * bt_stride;
+        for (int j = 0; j < P; ++j) mem = mem && bt[j] == casc[1 + j];
+    }
+    if (!__any(mem)) return;  // whole wave: no member row
+
+    bf16x8 qf[4];
+    {
+        const int nh = RP ? hq + 2 * hkv : hq;
+        const uint16_t* qp = q + ((int64_t)(mem ? seq : 0) * nh + head) * kD + 8 * h4;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) qf[c] = *reinterpret_cast<const bf16x8*>(qp + 32 * c);
+        if constexpr (RP) {
+            const float* cs = cos_sin + (int64_t)(mem ? pos[seq] : 0) * kD;
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const int d0 = 32 * c + 8 * h4;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const float co = cs[d0 + j], si = cs[64 + d0 + j];
+                    const float x1 = (float)qf[c][j], x2 = (float)qf[c + 2][j];
+                    qf[c][j] = (__bf16)(x1 * co - x2 * si);
+                    qf[c + 2][j] = (__bf16)(x2 * co + x1 * si);
+                }
+            }
+        }
+        if (!mem) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) qf[c] = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        }
+    }
+
+    float m = -1e30f, lsum = 0.f;
+    f32x4 o[8];
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t0 = 0; t0 < L; t0 += 32) {
+        // pages A (tokens t0 .. +15) and B (+16 .. +31); past the prefix B re-reads A (masked below)
+        const int64_t blkA = casc[1 + t0 / block_size];
+        const int64_t blkB = t0 + block_size < L ? casc[2 + t0 / block_size] : blkA;
+        bf16x8 kf[2][4], vf[8];
+        const int64_t kblk = r < 8 ? blkA : blkB;
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            const int off = (8 * (r >> 2) + 4 * g + (r & 3)) & (block_size - 1);
+            const int64_t koff = (((kblk * hkv + h) * block_size) + off) * kD + 8 * h4;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) kf[g][c] = *reinterpret_cast<const bf16x8*>(kc + koff + 32 * c);
+        }
+        const int64_t vblk = h4 < 2 ? blkA : blkB;
+        const int64_t voff = ((vblk * hkv + h) * kD) * (int64_t)block_size + 8 * (h4 & 1);
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt)
+            vf[dt] = *reinterpret_cast<const bf16x8*>(vc + voff + (int64_t)(dt * 16 + r) * block_size);
+        f32x4 sc[2];
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[g][c], qf[c], acc, 0, 0, 0);
+            sc[g] = acc;
+        }
+        // lane (r, h4): S^T token 8 h4 + 4 g + i of row r; PV operand element j = token 8 h4 + j (decode kernel map)
+        if (t0 + 32 > L) {
+            const int lim = L - (t0 + 8 * h4);
+#pragma unroll
+            for (int g = 0; g < 2; ++g)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) sc[g][i] = (4 * g + i) >= lim ? -INFINITY : sc[g][i];
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                if (j >= lim)
+#pragma unroll
+                    for (int dt = 0; dt < 8; ++dt) vf[dt][j] = (__bf16)0.f;
+        }
+        float mx = -INFINITY;
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) mx = fmaxf(mx, sc[g][i]);
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * scale_log2;
+        const float mnew = fmaxf(m, mx);
+        const float alpha = exp2f(m - mnew);
+        m = mnew;
+        float ps = 0.f;
+        bf16x8 pf;
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float p = exp2f(fmaf(sc[g][i], scale_log2, -m));
+                ps += p;
+                pf[4 * g + i] = (__bf16)p;
+            }
+        lsum = lsum * alpha + ps;
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) {
+            o[dt] *= alpha;
+            o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[dt], pf, o[dt], 0, 0, 0);
+        }
+    }
+    float lt = lsum;
+    lt += __shfl_xor(lt, 16, 64);
+    lt += __shfl_xor(lt, 32, 64);
+    if (mem) {
+        const int64_t row = (int64_t)seq * hq + head;
+        const float inv = 1.f / lt;  // lt >= 1: the row's max key contributes 2^0
+        uint16_t* op = opre + row * kD + 4 * h4;
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) {
+            u16x4 ov;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) ov[i] = f2bf(o[dt][i] * inv);
+            *reinterpret_cast<u16x4*>(op + 16 * dt) = ov;
+        }
+        if (h4 == 0) lpre[row] = m + __log2f(lt);
+    }
+}
+
 // Fused decode step (RP): RoPE + paged-KV write + one-wave-per-(seq, kv head) attention.  Returns false (nothing
 // launched) off the shapes the one-wave kernel serves; the caller then runs rope_kv_write + launch_paged_attn.
 bool launch_decode_attn_rope(const uint16_t* qkv, const int32_t* pos, const float* cos_sin, void* kc, void* vc,
                              const int32_t* block_table, int bt_stride, const int32_t* ctx_len, uint16_t* out, int n,
-                             int hq, int hkv, int block_size, float scale, hipStream_t st) {
+                             int hq, int hkv, int block_size, float scale, hipStream_t st, const int32_t* casc,
+                             uint16_t* opre, float* lpre) {
     const int nitems = n * hkv;
     if (n == 0 || hq / hkv > 16 || block_size != 16 || nitems < 2048 || knob("decode_attn_legacy", 0) ||
         knob("decode_pf", 0) || !knob("decode_lean", 1) || !knob("decode_rope_fused", 1))
         return false;
     const float scale_log2 = scale * 1.4426950408889634f;
+    if (casc != nullptr) {  // the shared-prefix part first; the decode kernel merges it
+        const int G = hq / hkv;
+        const dim3 grid((n + 4 * (16 / G) - 1) / (4 * (16 / G)), hkv);
+        hipLaunchKernelGGL(casc_prefix_kernel<true>, grid, dim3(256), 0, st, qkv, (const uint16_t*)kc,
+                           (const uint16_t*)vc, casc, block_table, bt_stride, ctx_len, opre, lpre, n, hq, hkv,
+                           scale_log2, CHRONOS_GATE, pos, cos_sin);
+    }
     if (!knob("decode_klds", 1))
         hipLaunchKernelGGL((paged_decode_kernel<false, false, true, 3, true, false>), dim3((nitems + 3) / 4),
                            dim3(256), 0, st, qkv, kc, vc, block_table, bt_stride, ctx_len, out, nitems, hq, hkv,
-                           scale_log2, 1.f, 1.f, CHRONOS_GATE, pos, cos_sin);
+                           scale_log2, 1.f, 1.f, CHRONOS_GATE, pos, cos_sin, casc, opre, lpre);
     else if (knob("decode_occ3", 1))
         hipLaunchKernelGGL((paged_decode_kernel<false, false, true, 3, true>), dim3((nitems + 3) / 4), dim3(256), kPdKlds,
                            st, qkv, kc, vc, block_table, bt_stride, ctx_len, out, nitems, hq, hkv, scale_log2, 1.f,
-                           1.f, CHRONOS_GATE, pos, cos_sin);
+                           1.f, CHRONOS_GATE, pos, cos_sin, casc, opre, lpre);
     else
         hipLaunchKernelGGL((paged_decode_kernel<false, false, true, 1, true>), dim3((nitems + 3) / 4), dim3(256), kPdKlds,
                            st, qkv, kc, vc, block_table, bt_stride, ctx_len, out, nitems, hq, hkv, scale_log2, 1.f,
-                           1.f, CHRONOS_GATE, pos, cos_sin);
+                           1.f, CHRONOS_GATE, pos, cos_sin, casc, opre, lpre);
     return true;
 }
 

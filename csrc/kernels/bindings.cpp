@@ -30,7 +30,8 @@ void launch_rope_kv_write(const uint16_t*, const int32_t*, const int32_t*, const
 void launch_silu_mul(const uint16_t*, uint16_t*, int64_t, int, hipStream_t);
 size_t paged_attn_smem(int nqt);
 bool launch_decode_attn_rope(const uint16_t*, const int32_t*, const float*, void*, void*, const int32_t*, int,
-                             const int32_t*, uint16_t*, int, int, int, int, float, hipStream_t);
+                             const int32_t*, uint16_t*, int, int, int, int, float, hipStream_t, const int32_t*,
+                             uint16_t*, float*);
 void launch_paged_attn(const uint16_t*, const void*, const void*, const int32_t*, int, const int32_t*,
                        const int32_t*, const int32_t*, int, int, int, uint16_t*, float*, float*, int, int, int, float,
                        bool, float, float, hipStream_t);
@@ -195,9 +196,13 @@ void rope_kv_write(const Tensor& qkv, const Tensor& pos, const Tensor& tok_seq, 
 // Returns the [n, hq, 128] attention output, or an empty tensor when the fused kernel does not serve this shape (the
 // caller then runs rope_kv_write + paged_attention).  Decode rows only: row i is sequence i, its one token at pos[i]
 // is the last of its context (ctx_len[i] == pos[i] + 1).
+// casc (optional, int32 [1 + P_max] on the device: P, then the shared prefix's block ids) with casc_o (bf16 [>= n, hq,
+// 128]) and casc_l (f32 [>= n, hq]) scratch: cascade attention over the shared prefix (attention.hip
+// casc_prefix_kernel) merged into the decode kernel.  casc[0] = 0 turns it off without re-capturing a graph.
 Tensor decode_attention_rope(const Tensor& qkv, const Tensor& pos, const Tensor& cos_sin, const Tensor& k_cache,
                              const Tensor& v_cache, const Tensor& block_table, const Tensor& ctx_len, int64_t n,
-                             int64_t hq, double scale) {
+                             int64_t hq, double scale, const c10::optional<Tensor>& casc,
+                             const c10::optional<Tensor>& casc_o, const c10::optional<Tensor>& casc_l) {
     chk_bf16(qkv, "qkv");
     chk_i32(pos, "pos");
     chk_i32(block_table, "block_table");
@@ -214,10 +219,26 @@ Tensor decode_attention_rope(const Tensor& qkv, const Tensor& pos, const Tensor&
         "k_cache [NB, hkv, BS, 128], v_cache [NB, hkv, 128, BS]");
     c10::hip::HIPGuardMasqueradingAsCUDA g(qkv.device());
     if (fp8) return at::empty({0}, qkv.options());
+    const int32_t* cp = nullptr;
+    uint16_t* co = nullptr;
+    float* cl = nullptr;
+    if (casc.has_value()) {
+        chk_i32(*casc, "casc");
+        CHK(casc_o.has_value() && casc_l.has_value(), "casc needs casc_o and casc_l");
+        chk_bf16(*casc_o, "casc_o");
+        chk_gpu(*casc_l, "casc_l");
+        CHK(casc->numel() >= 2 && casc->numel() <= 65, "casc: [1 + P_max], P_max <= 64");
+        CHK(casc_o->numel() >= n * hq * 128 && casc_l->scalar_type() == at::kFloat && casc_l->numel() >= n * hq,
+            "casc_o [>= n, hq, 128] bf16, casc_l [>= n, hq] f32");
+        cp = i32(*casc);
+        co = bfm(*casc_o);
+        cl = casc_l->data_ptr<float>();
+    }
     auto out = at::empty({n, hq, 128}, qkv.options());
     if (!chronos::launch_decode_attn_rope(bf(qkv), i32(pos), cos_sin.data_ptr<float>(), k_cache.data_ptr(),
                                           v_cache.data_ptr(), i32(block_table), (int)block_table.size(1), i32(ctx_len),
-                                          bfm(out), (int)n, (int)hq, (int)hkv, (int)bs, (float)scale, cur_stream()))
+                                          bfm(out), (int)n, (int)hq, (int)hkv, (int)bs, (float)scale, cur_stream(),
+                                          cp, co, cl))
         return at::empty({0}, qkv.options());
     return out;
 }
@@ -805,7 +826,8 @@ TORCH_LIBRARY(chronos, m) {
     m.def("ar_capacity(int h) -> int", &ar_capacity);
     m.def("ar_destroy(int h) -> ()", &ar_destroy);
     m.def("decode_attention_rope(Tensor qkv, Tensor pos, Tensor cos_sin, Tensor(a!) k_cache, Tensor(b!) v_cache, "
-          "Tensor block_table, Tensor ctx_len, int n, int hq, float scale) -> Tensor");
+          "Tensor block_table, Tensor ctx_len, int n, int hq, float scale, Tensor? casc=None, Tensor(c!)? casc_o=None, "
+          "Tensor(d!)? casc_l=None) -> Tensor");
     m.def("paged_attention(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_table, Tensor q_start, "
           "Tensor ctx_len, Tensor? tiles, int ntiles, int nqt, int nsplit, float scale, float k_scale=1.0, "
           "float v_scale=1.0) -> Tensor");

@@ -122,6 +122,14 @@ class EngineConfig:
     # profiles/r3_bench_mixed_ab.txt).  A closed loop's harvests return ~100 completions (and as many arrivals) at
     # once; a limit of 64 turned most of them back into plain prefill steps (619 chains/s).
     mixed_max_backlog: int = 256
+    # Cascade decode attention (csrc/kernels/attention.hip casc_prefix_kernel): when at least cascade_min_rows running
+    # sequences hold the same leading prefix-cache blocks (the shared prompt template), their decode attention over
+    # those blocks runs once per 16 / G rows as an MFMA pass and is merged into each row's walk over its own tokens.
+    # Off by default: measured slower on the MI355X (profiles/r5/cascade_ab.md: the shared blocks are L2 hits for
+    # the one-wave kernel, so skipping them saves little, and the extra pass costs ~10 us per layer at 1024 rows).
+    cascade: bool = False
+    cascade_min_rows: int = 32
+    cascade_max_blocks: int = 8
     # token automata compiled at start-up (a first request must not pay the ~4 s vocab walk: the reference's cold-start
     # timeout): "verdict" = the CHRONOS verdict schema the sensor sends, "json" = format:"json"
     warm_formats: tuple = ("verdict", "json")
@@ -294,6 +302,14 @@ class Engine:
         self._snap_seq = 0
         self._pending: Optional[_Snapshot] = None
         self._deferred: list = []  # (request, reason) harvested, finished after the next launch (_flush_deferred)
+        # cascade prefix state: device [P, block ids...] read by the decode graph, its O / lse scratch, host copy
+        self._casc = None
+        self._casc_cur: tuple = ()
+        if self.device.type == "cuda" and cfg.cascade and self.model.hq % self.model.hkv == 0 and \
+                16 % (self.model.hq // self.model.hkv) == 0:
+            self._casc = (torch.zeros(1 + cfg.cascade_max_blocks, dtype=torch.int32, device=dev),
+                          torch.empty(S, self.model.hq, 128, dtype=torch.bfloat16, device=dev),
+                          torch.empty(S, self.model.hq, dtype=torch.float32, device=dev))
         self._async = cfg.async_harvest
         if self.device.type == "cuda":
             self._warmup()
@@ -471,7 +487,10 @@ class Engine:
         self.free_slots = list(range(S - 1, -1, -1))
         self.blocks = BlockManager(self.blocks.num_blocks, self.blocks.block_size,
                                    prefix_cache=self.blocks.prefix_cache, partial_prefix=self.cfg.partial_prefix)
+        self._casc_cur = ()
         try:
+            if self._casc is not None:
+                self._casc[0].zero_()
             self.s_state.fill_(-1)
             self.s_bt.zero_()
             self.s_pos.zero_()
@@ -541,6 +560,7 @@ class Engine:
                     self.blocks.release([part[0]])  # its reference took an evictable block out of the free pool
                     part = None
                 req.blocks = shared + self.blocks.alloc(nblk - len(shared))
+                req.meta["casc_n"] = len(shared)  # leading blocks shared through the prefix cache (cascade candidates)
                 req.prefilled = len(shared) * self.blocks.block_size
                 self.blocks.note_prompt(req.prompt_ids, req.blocks, len(shared))
                 if part is not None:  # the first j slots of block len(shared) come from a computed block
@@ -656,6 +676,32 @@ class Engine:
         self.stats["preemptions"] += 1
         with self._lock:
             self.waiting.appendleft(r)
+
+    def _update_casc(self) -> None:
+        """Pick the cascade prefix for the next decode launch: the longest run of leading blocks held by at least
+        cascade_min_rows sequences (block refcounts), taken from the latest running requests that share prefix-cache
+        blocks.  Re-evaluated every launch (a few dozen dictionary lookups); the device copy is rewritten only on a
+        change.  Rows that do not hold the prefix are unaffected (both kernels test membership per row)."""
+        if self._casc is None:
+            return
+        ref, mn, pmax = self.blocks._ref, self.cfg.cascade_min_rows, self.cfg.cascade_max_blocks
+        new: tuple = ()
+        for r in list(self.running.values())[-32:]:  # the latest admissions (a wave's all share the template)
+            k = min(r.meta.get("casc_n", 0), pmax, len(r.blocks))
+            if k <= len(new):
+                continue
+            p = 0
+            while p < k and ref.get(r.blocks[p], 0) >= mn:
+                p += 1
+            if p > len(new):
+                new = tuple(r.blocks[:p])
+        if new == self._casc_cur:
+            return
+        self._casc_cur = new
+        v = [len(new)] + list(new) + [0] * (pmax - len(new))
+        self._casc[0].copy_(h2d(torch.tensor(v, dtype=torch.int32), self.device))
+        self.stats["cascade_updates"] += 1
+        self.stats["cascade_max_blocks"] = max(self.stats["cascade_max_blocks"], len(new))
 
     def _free_slots(self, slots: list) -> None:
         """Return slots to the free list and park their device state (empty, scratch block table)."""
@@ -818,8 +864,9 @@ class Engine:
         sb = make_prefill_batch(chunks, starts, bts, self.model.cfg, self.tp, self.device,
                                 max_blocks=self.max_blocks_per_seq, nqt=self.cfg.prefill_nqt)
         tp_, bp = sum(len(c) for c in chunks), len(chunks)
+        self._update_casc()
         sb.dec = StepBatch(self.s_ids[:n], self.s_pos[:n], self.ar[:n], self.s_bt[:n], self.ar[:n + 1], self.s_ctx[:n],
-                           self.ar64[:n], None, n, 1, self._nsplit(n, self._ctx_class()))
+                           self.ar64[:n], None, n, 1, self._nsplit(n, self._ctx_class()), casc=self._casc)
         sb.last_idx = torch.cat([sb.last_idx, tp_ + self.ar64[:n]])
         logits = self.model.forward(sb, self.kv)
         done_rows, done_reqs = self._prefill_done(reqs, chunks)
@@ -858,7 +905,7 @@ class Engine:
 
     def _decode_once(self, n: int, nsplit: int) -> None:
         sb = StepBatch(self.s_ids[:n], self.s_pos[:n], self.ar[:n], self.s_bt[:n], self.ar[:n + 1], self.s_ctx[:n],
-                       self.ar64[:n], None, n, 1, nsplit)
+                       self.ar64[:n], None, n, 1, nsplit, casc=self._casc)
         logits = self.model.forward(sb, self.kv)
         ops.constrained_sample(logits, None, self.bank.next, self.bank.dist, DONE, self.s_state[:n], self.s_rem[:n],
                                self.s_temp[:n], self.s_seed[:n], self.s_ids[:n], self.s_pos[:n], self.s_ctx[:n],
@@ -897,6 +944,7 @@ class Engine:
         self._grow_for(k)  # (may preempt: the bucket is sized after it)
         if not self.running:
             return None
+        self._update_casc()
         n = min(self._decode_rows(), self.cfg.max_slots)
         ns = self._nsplit(n, self._ctx_class())
         if self.device.type == "cuda" and self.cfg.use_graphs:

@@ -484,6 +484,9 @@ class StepBatch:
     # mixed step: decode rows (a decode-mode StepBatch over device slot state) appended after this batch's prefill
     # tokens — one forward, shared projections; ``last_idx`` then also lists the decode rows (after the prefill rows)
     dec: Optional["StepBatch"] = None
+    # decode rows: cascade attention over a shared prompt prefix (ops.decode_attention_rope ``casc``), device tensors
+    # owned by the engine and updated in place between graph replays
+    casc: Optional[tuple] = None
 
 
 def make_prefill_batch(prompts: list[list[int]], starts: list[int], block_tables: list[list[int]], cfg: LlamaConfig,
@@ -540,7 +543,7 @@ def h2d(t: torch.Tensor | None, device) -> torch.Tensor | None:
 def to_device(sb: StepBatch, device) -> StepBatch:
     mv = lambda t: h2d(t, device)  # noqa: E731
     return StepBatch(mv(sb.ids), mv(sb.pos), mv(sb.tok_seq), mv(sb.block_table), mv(sb.q_start), mv(sb.ctx_len),
-                     mv(sb.last_idx), mv(sb.tiles), sb.ntiles, sb.nqt, sb.nsplit, sb.parts, sb.cp, sb.dec)
+                     mv(sb.last_idx), mv(sb.tiles), sb.ntiles, sb.nqt, sb.nsplit, sb.parts, sb.cp, sb.dec, sb.casc)
 
 
 # -----------------------------------------------------------------------------------------------------------------
@@ -595,7 +598,7 @@ class LlamaModel:
         if _FUSE_DECODE_ROPE and sb.tiles is None and sb.cp is None and sb.nqt == 1 and sb.nsplit == 1:
             # batched decode: RoPE + KV write inside the one-wave decode attention (None off its shapes)
             attn = ops.decode_attention_rope(qkv, sb.pos, self.cos_sin, kv.k[li], kv.v[li], sb.block_table,
-                                             sb.ctx_len, T, self.hq, self.scale)
+                                             sb.ctx_len, T, self.hq, self.scale, sb.casc)
         if attn is None:
             ops.rope_kv_write(qkv, sb.pos, sb.tok_seq, sb.block_table, self.cos_sin, q_buf, kv.k[li], kv.v[li],
                               self.hq, self.hkv, True, kv.k_scale[li], kv.v_scale[li])

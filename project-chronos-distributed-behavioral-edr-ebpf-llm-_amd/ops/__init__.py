@@ -224,11 +224,16 @@ def paged_attention(q, k_cache, v_cache, block_table, q_start, ctx_len, tiles=No
 
 
 def decode_attention_rope(qkv, pos, cos_sin, k_cache, v_cache, block_table, ctx_len, n: int, hq: int,
-                          scale: float):
+                          scale: float, casc=None):
     """Decode step (row i = sequence i, one token at pos[i], ctx_len[i] == pos[i] + 1): RoPE + paged-KV write + paged
     attention in one launch (csrc/kernels/attention.hip paged_decode_kernel RP).  Returns the [n, hq, 128] output, or
     None when the fused kernel does not serve the shape (fp8 KV, < 2048 (row, kv head) items, ...): the caller then
-    runs rope_kv_write + paged_attention, which compute the same thing."""
+    runs rope_kv_write + paged_attention, which compute the same thing.
+
+    ``casc``: optional (casc [1 + P_max] int32, o scratch [S, hq, 128] bf16, lse scratch [S, hq] f32) — cascade
+    attention over a shared prompt prefix (casc[0] = P blocks, then their ids): rows whose block table starts with
+    those blocks attend the prefix in one MFMA pass per 16 / G rows and merge it into the walk over their own tokens
+    (csrc/kernels/attention.hip casc_prefix_kernel).  Mathematically the same attention; casc[0] = 0 disables it."""
     if not qkv.is_cuda:
         return None
     if _checking(qkv):
@@ -236,7 +241,16 @@ def decode_attention_rope(qkv, pos, cos_sin, k_cache, v_cache, block_table, ctx_
         _need(bool((c == p + 1).all()), "decode_attention_rope: ctx_len must be pos + 1 (decode rows)")
         _need(bool(((p >= 0) & (p < cos_sin.shape[0])).all()), "decode_attention_rope: position outside the rope table")
         _check_paged(block_table, k_cache, torch.arange(n), c, "decode_attention_rope")
-    out = _k().decode_attention_rope(qkv, pos, cos_sin, k_cache, v_cache, block_table, ctx_len, n, hq, scale)
+        if casc is not None:
+            cv = casc[0].cpu().long()
+            P = int(cv[0])
+            _need(0 <= P < cv.numel(), "decode_attention_rope: cascade prefix length")
+            _need(bool(((cv[1:1 + P] >= 0) & (cv[1:1 + P] < k_cache.shape[0])).all()), "cascade block id out of range")
+    if casc is not None:
+        out = _k().decode_attention_rope(qkv, pos, cos_sin, k_cache, v_cache, block_table, ctx_len, n, hq, scale,
+                                         casc[0], casc[1], casc[2])
+    else:
+        out = _k().decode_attention_rope(qkv, pos, cos_sin, k_cache, v_cache, block_table, ctx_len, n, hq, scale)
     return out if out.numel() else None
 
 

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--gm", type=int, default=8)
+    ap.add_argument("--gms", default="", help="also time every w4 variant at these tile-group sizes")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     lib = ctypes.CDLL(os.path.abspath(a.lib))
@@ -35,9 +36,12 @@ def main():
 
         ops.load()
     dev = "cuda"
-    big = [(8192, 8192, 8192), (16384, 6144, 4096), (16384, 4096, 4096), (16384, 28672, 4096), (16384, 4096, 14336)]
+    if a.shapes == "sq":
+        big = [(8192, 8192, 8192), (16384, 28672, 4096)]
+    else:
+        big = [(8192, 8192, 8192), (16384, 6144, 4096), (16384, 4096, 4096), (16384, 28672, 4096), (16384, 4096, 14336)]
     dec = [(1024, 6144, 4096), (1024, 4096, 4096), (1024, 28672, 4096), (1024, 4096, 14336), (1024, 128256, 4096)]
-    shapes = {"big": big, "decode": dec, "all": big + dec}[a.shapes]
+    shapes = {"big": big, "sq": big, "decode": dec, "all": big + dec}[a.shapes]
     vars_ = [int(v) for v in a.vars.split(",") if v]
     lgs = [int(v) for v in a.lg.split(",") if v]
     g = torch.Generator(device=dev).manual_seed(0)
@@ -50,12 +54,14 @@ def main():
         st = torch.cuda.current_stream().cuda_stream
         ref = (x.float() @ ws[0].float().t())
         fns = {"lib": lambda w: torch.matmul(x, w.t())}
+        gms = [a.gm] + [int(q) for q in a.gms.split(",") if q]
         for v in vars_:
-            def f(w, v=v):
-                rc = lib.gemm_w4(x.data_ptr(), w.data_ptr(), y.data_ptr(), M, N, K, v, a.gm, st)
-                assert rc == 0, rc
-                return y
-            fns[f"w4v{v}"] = f
+            for gmv in gms:
+                def f(w, v=v, gmv=gmv):
+                    rc = lib.gemm_w4(x.data_ptr(), w.data_ptr(), y.data_ptr(), M, N, K, v, gmv, st)
+                    assert rc == 0, rc
+                    return y
+                fns[f"w4v{v}" + (f"g{gmv}" if gmv != a.gm else "")] = f
         for c in lgs:
             fns[f"lg{c}"] = lambda w, c=c: torch.ops.chronos.gemm_pp(x, w, 0, c, 1, None, None, 1e-5, False)[0]
         errs = {}
