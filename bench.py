@@ -60,8 +60,9 @@ def parse():
     ap.add_argument("--async-harvest", action="store_true")
     ap.add_argument("--cascade", action="store_true", help="shared-prefix cascade decode attention (off: measured "
                     "slower, profiles/r5/cascade_ab.md)")
-    ap.add_argument("--kv-alloc", choices=["lazy", "full"], default="lazy",
-                    help="KV reservation at admission (lazy: prompt + lookahead, grown per launch, preemption)")
+    ap.add_argument("--kv-alloc", choices=["auto", "lazy", "full"], default="auto",
+                    help="KV reservation at admission (lazy: prompt + lookahead, grown per launch, preemption; auto: "
+                         "full when the pool holds every slot at max length)")
     ap.add_argument("--prefill-ramp", type=int, default=2048, help="first prefill step after idle (0 = full chunks)")
     ap.add_argument("--no-jump-forward", action="store_true", help="decode grammar-forced runs token by token")
     ap.add_argument("--jump-max-rows", type=int, default=None,

@@ -41,6 +41,34 @@ __device__ __forceinline__ void w4_dma_asm(const __amdgpu_buffer_rsrc_t& r, uint
                  : "memory");
 }
 
+
+// Tile order.  gm < 256: groups of gm M-tiles sweeping all N tiles (gemm_lg's order).  gm = g | SM << 8 | SN << 16:
+// the tile grid is cut into SM x SN super-blocks (one XCD's share of consecutive logical tiles after xcd_remap), each
+// walked in groups of g M-tiles x SN N-tiles — so an XCD's L2 sees a near-square block of x and W tiles (fewer
+// MALL / HBM bytes than a strip of all N tiles), and the ~32 tiles it runs together share g x tiles and SN W tiles.
+// Tiles past the last whole super-block row / column fall back to the plain group order.
+__device__ __forceinline__ void w4_tile_map(int tile, int mt, int ntl, int gm, int& tm, int& tn) {
+    const int g = gm & 0xff, SM = (gm >> 8) & 0xff, SN = gm >> 16;
+    if (SM > 0 && SN > 0 && mt % SM == 0 && ntl % SN == 0 && SM % g == 0) {
+        const int per = SM * SN, sup = tile / per, sub = tile - sup * per;
+        const int sbm = mt / SM;  // super-blocks along M
+        const int sm0 = (sup % sbm) * SM, sn0 = (sup / sbm) * SN;
+        const int gper = g * SN, gi = sub / gper, r = sub - gi * gper;
+        tm = sm0 + gi * g + r % g;
+        tn = sn0 + r / g;
+        return;
+    }
+    if (g > 0 && mt > g) {
+        const int per = g * ntl, grp = tile / per, r = tile - grp * per;
+        const int gsz = min(g, mt - grp * g);
+        tm = grp * g + r % gsz;
+        tn = r / gsz;
+    } else {
+        tm = tile % mt;
+        tn = tile / mt;
+    }
+}
+
 // VAR bit 1: DMA as inline asm (hipcc adds no lgkmcnt wait in front of it); bit 2: MFMA in inline asm with the
 // accumulator pinned to AGPRs ("+a"); bit 4: issue order written out and pinned by sched_barrier(0) (else
 // sched_group_barrier interleave, which cannot see asm MFMAs); bit 8: (pinned) DMA pieces at the head of k-step B
@@ -67,15 +95,7 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(const uint16_t* __restr
     const int mt = (M + XM - 1) / XM, ntl = (N + WN - 1) / WN;
     const int tile = xcd_remap(blockIdx.x, mt * ntl);
     int tm, tn;
-    if (gm > 0 && mt > gm) {
-        const int per = gm * ntl, grp = tile / per, r = tile - grp * per;
-        const int gsz = min(gm, mt - grp * gm);
-        tm = grp * gm + r % gsz;
-        tn = r / gsz;
-    } else {
-        tm = tile % mt;
-        tn = tile / mt;
-    }
+    w4_tile_map(tile, mt, ntl, gm, tm, tn);
     const int m0 = tm * XM, n0 = tn * WN;
     const int NS = K / 64;
 
@@ -309,15 +329,7 @@ __global__ void __launch_bounds__(256, 1) gemm_w4b_kernel(const uint16_t* __rest
     const int mt = (M + XM - 1) / XM, ntl = (N + WN - 1) / WN;
     const int tile = xcd_remap(blockIdx.x, mt * ntl);
     int tm, tn;
-    if (gm > 0 && mt > gm) {
-        const int per = gm * ntl, grp = tile / per, r = tile - grp * per;
-        const int gsz = min(gm, mt - grp * gm);
-        tm = grp * gm + r % gsz;
-        tn = r / gsz;
-    } else {
-        tm = tile % mt;
-        tn = tile / mt;
-    }
+    w4_tile_map(tile, mt, ntl, gm, tm, tn);
     const int m0 = tm * XM, n0 = tn * WN;
     const int NS = K / 64, NS1 = NS - 1;
 

@@ -3,7 +3,8 @@
 Replaces what Ollama + llama.cpp did for the reference:
 
 * **admission**: a request gets a decode *slot* and the KV blocks of its prompt plus ``kv_lookahead`` generated
-  tokens (``kv_alloc="lazy"``, the default; ``"full"`` reserves prompt + num_predict up front as rounds 1-4 did).
+  tokens (``kv_alloc="lazy"``; ``"full"`` reserves prompt + num_predict up front as rounds 1-4 did; the default
+  ``"auto"`` is full when the pool can hold every slot at max_model_len, lazy when it cannot).
   KV is sized from the HBM budget (288 GB per MI355X — 1-2 M tokens for 8B, SURVEY.md App. C);
 * **KV growth and preemption** (SURVEY.md §7.2 step 6): before every launch that writes generated-token KV (decode
   burst, mixed step, jump-forward) each running sequence's blocks are grown to cover the positions that launch can
@@ -88,8 +89,10 @@ class EngineConfig:
     async_harvest: bool = False    # harvest burst k while burst k+1 runs (hides host work, delays compaction)
     request_timeout_s: float = 0.0  # >0: a request not finished this long after submit is cancelled (reason "timeout")
     # KV reservation: "lazy" = prompt + kv_lookahead tokens at admission, grown per launch, recompute preemption of the
-    # newest sequences when the pool runs dry; "full" = prompt + num_predict at admission (never preempts)
-    kv_alloc: str = "lazy"
+    # newest sequences when the pool runs dry; "full" = prompt + num_predict at admission (never preempts); "auto" =
+    # full when the pool holds every slot at max_model_len (no pressure is possible: the per-launch growth bookkeeping
+    # would be pure host overhead, ~0.4 % on the headline wave), lazy otherwise
+    kv_alloc: str = "auto"
     kv_lookahead: int = 64         # generated-token headroom allocated per growth (amortises the block-table updates)
     kv_watermark: float = 0.01     # lazy admission leaves this fraction of the pool free for the running rows' growth
     tp_overlap: bool = True        # TP prefill: two micro-batches, each one's RCCL all-reduces overlap the other's compute
@@ -260,6 +263,9 @@ class Engine:
                 dist.all_reduce(t, op=dist.ReduceOp.MIN, group=grp.group)
                 nb = int(t.item())
         self.kv = KVCache(mc, self.tp, nb, bs, self.device, cfg.kv_dtype, cfg.kv_scale, cfg.kv_scale)
+        if cfg.kv_alloc not in ("auto", "lazy", "full"):
+            raise ValueError(f"kv_alloc must be auto, lazy or full, not {cfg.kv_alloc!r}")
+        self.kv_alloc = cfg.kv_alloc if cfg.kv_alloc != "auto" else ("full" if nb >= need else "lazy")
         self.blocks = BlockManager(nb, bs, prefix_cache=cfg.prefix_cache, partial_prefix=cfg.partial_prefix)
         # ---- slot state (device) ----
         S, dev = cfg.max_slots, self.device
@@ -581,7 +587,7 @@ class Engine:
 
     def _admit_blocks(self, req: Request) -> tuple[int, int]:
         """(KV blocks a request takes at admission, free blocks lazy admission leaves for the running rows)."""
-        if self.cfg.kv_alloc == "full":
+        if self.kv_alloc == "full":
             return self.blocks.blocks_for(req.kv_cap), 0
         toks = min(req.kv_cap, len(req.prompt_ids) + self.cfg.kv_lookahead)
         return self.blocks.blocks_for(toks), int(self.cfg.kv_watermark * self.blocks.num_blocks)
@@ -716,7 +722,7 @@ class Engine:
     def _grow_for(self, k: int) -> None:
         """Lazy KV: every running row may write k more KV positions in the launch about to be queued (a decode burst
         of k steps, or a mixed step's one): grow whoever needs it, then advance the bound."""
-        if self.cfg.kv_alloc != "lazy" or not self.running:
+        if self.kv_alloc != "lazy" or not self.running:
             return
         bs = self.blocks.block_size
         extra = [(r, r.pos_hi + k) for r in self.running.values()
@@ -1123,7 +1129,7 @@ class Engine:
         if unpark:
             self.s_state[dv(torch.tensor([u[0] for u in unpark], dtype=torch.int64))] = dv(
                 torch.tensor([u[1] for u in unpark], dtype=torch.int32))
-        if rows and self.cfg.kv_alloc == "lazy":
+        if rows and self.kv_alloc == "lazy":
             # the forward writes positions pos0 .. pos0 + k: grow (preempting the newest rows if the pool is short)
             self._ensure_kv([(r, len(r.prompt_ids) + n0 + k) for r, _, _, n0, k in rows])
             rows = [x for x in rows if self.running.get(x[0].slot) is x[0]]

@@ -84,7 +84,7 @@ def candidates(m, n, k, mode, keep=6):
     # the software-pipelined family (gemm_lg.hip): every slab / ring config that tiles the shape, split-K where the
     # tile grid under-fills the chip
     if m >= 256:
-        for cfg in (20, 29, 30, 19, 31, 23):
+        for cfg in (20, 29, 30, 19, 31, 23, 76, 77):
             bm, bn = G._PP_BM[cfg], G._PP_BN[cfg]
             tiles = -(-m // bm) * -(-n // bn)
             for sk in (1, 2, 4):
@@ -131,6 +131,7 @@ def main():
     ap.add_argument("--out-plan", default="")
     ap.add_argument("--out-table", default="")
     ap.add_argument("--merge", default="", help="plan file whose rows at M not measured in this run are kept")
+    ap.add_argument("--ops", default="", help="only these projections (e.g. qkv,lm_head)")
     ap.add_argument("--fp8", action="store_true", help="tune the W8A8 fp8 routing (qplans) instead of the bf16 plan")
     args = ap.parse_args()
     merged = {}
@@ -149,6 +150,8 @@ def main():
     st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for model in args.models.split(","):
         for op, (n, k, mode) in SHAPES[model].items():
+            if args.ops and op not in args.ops.split(","):
+                continue
             g = torch.Generator(device=dev).manual_seed(0)
             ncopy = max(2, -(-(600 << 20) // (n * k * 2)))
             ws = [((torch.rand(n, k, device=dev, generator=g) * 2 - 1) * 0.05).to(torch.bfloat16)

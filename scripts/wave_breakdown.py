@@ -20,8 +20,11 @@ def cls(n):
 
 
 def main(path):
-    rows = list(csv.DictReader(gzip.open(path, "rt")))
+    rows = list(csv.DictReader(gzip.open(path, "rt") if path.endswith(".gz") else open(path)))
     for r in rows:
+        if "Kernel_Name" in r:  # a raw rocprofv3 kernel_trace.csv
+            r.update(name=r["Kernel_Name"], start=r["Start_Timestamp"], end=r["End_Timestamp"],
+                     grid=r["Grid_Size_X"], wg=r["Workgroup_Size_X"])
         r["s"], r["e"] = int(r["start"]), int(r["end"])
     rows.sort(key=lambda r: r["s"])
     emb = [i for i, r in enumerate(rows) if "embedding_kernel" in r["name"]]

@@ -36,8 +36,10 @@ def _check(y, ref, tol=2e-2):
 
 
 LG = [12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 38, 39, 72, 73, 74, 75]
-# gemm_lg.hip configs (12-19 / 29-31 ring schedule, 20-28 slab schedule, 32-39 mid-M weight streaming)
-CFGS = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11] + LG
+# gemm_lg.hip configs (12-19 / 29-31 ring schedule, 20-28 slab schedule, 32-39 mid-M weight streaming); 76-77 (192 W
+# rows: plain epilogue only at these toy N, whose SwiGLU / residual widths are not multiples of 192)
+LG192 = [76, 77]
+CFGS = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11] + LG + LG192
 
 
 @pytest.mark.parametrize("cfg", CFGS)
@@ -51,7 +53,7 @@ def test_plain(cfg, m):
     _check(y, x.float() @ w.float().t())
 
 
-@pytest.mark.parametrize("cfg", [0, 3, 5, 8, 11] + LG)
+@pytest.mark.parametrize("cfg", [0, 3, 5, 8, 11] + LG + LG192)
 def test_n_tail(cfg):
     """N not a multiple of the tile (the 70B TP=8 LM-head shard is N = 16032): the last W tile is partial."""
     g = torch.Generator(device=DEV).manual_seed(21 + cfg)
@@ -63,7 +65,7 @@ def test_n_tail(cfg):
 
 
 @pytest.mark.parametrize("cfg,splitk", [(0, 2), (1, 4), (3, 2), (2, 5), (4, 2), (5, 4), (7, 2), (8, 2), (9, 4), (10, 2), (11, 5),
-                                        (12, 2), (13, 4), (14, 5), (15, 2), (16, 2), (17, 4), (18, 5), (19, 2), (20, 2), (21, 4), (22, 5), (23, 2), (24, 2), (25, 4), (26, 2), (27, 4), (28, 5), (29, 2), (30, 4), (31, 5), (32, 4), (33, 5), (34, 2), (35, 4), (36, 4), (37, 2), (38, 5), (39, 2), (72, 4), (73, 2), (74, 5), (75, 4)])
+                                        (12, 2), (13, 4), (14, 5), (15, 2), (16, 2), (17, 4), (18, 5), (19, 2), (20, 2), (21, 4), (22, 5), (23, 2), (24, 2), (25, 4), (26, 2), (27, 4), (28, 5), (29, 2), (30, 4), (31, 5), (32, 4), (33, 5), (34, 2), (35, 4), (36, 4), (37, 2), (38, 5), (39, 2), (72, 4), (73, 2), (74, 5), (75, 4), (76, 2), (77, 4)])
 def test_splitk(cfg, splitk):
     g = torch.Generator(device=DEV).manual_seed(11 + cfg)
     m, n, k = 300, 512, 64 * 20

@@ -86,3 +86,10 @@ def test_request_larger_than_cache_is_an_error_not_a_stall():
     eng.run_until_idle(max_steps=50)
     assert r.done_reason == "error" and "KV blocks" in (r.error or "")
     assert not eng.has_work()
+
+
+def test_auto_reservation_picks_by_pool_size():
+    """kv_alloc="auto": full reservation when the pool holds every slot at max_model_len (no pressure possible),
+    lazy growth + preemption when it does not."""
+    assert _engine(kv_alloc="auto").kv_alloc == "full"
+    assert _engine(kv_alloc="auto", kv_blocks=40).kv_alloc == "lazy"
