@@ -316,6 +316,305 @@ __global__ void __launch_bounds__(256, PF ? 2 : 1) paged_attn_kernel(
     if (!flag[0]) return;
     combine_tile<NQT>(part_o, part_lse, out, tile, h, rel0, qbase, qlen, hq, hkv, nsplit, gridDim.x);
 }
+
+// ------------------------------------------------------------------------------------------------------------------
+// Long-context decode with a kv split (flash-decoding; the 128k config): the split-over-waves
+// kernel above loads K straight into the MFMA layout (16 rows x 64 B per instruction) and V^T as 8-byte pieces, so
+// at 128k it issues 24 small loads per 32-token step and wave and runs at the address unit's rate, not HBM's: 125 us
+// per layer with bf16 KV and the same with fp8 (half the bytes, the same instructions).  Here every wave streams its
+// steps through a private LDS ring with lane-linear 1 KiB LDS-DMA pieces (bf16: 8 K + 8 V^T pieces per step, fp8:
+// 4 + 4 — the instruction count follows the bytes), NB steps in flight, and reads the MFMA fragments back with
+// conflict-free ds_reads (K chunks XOR-swizzled by row on the source address); fp8 converts with
+// v_cvt_scalef32_pk_bf16_fp8 (the cache scales folded into the score scale and the output).  The same token <->
+// operand map, softmax and four-wave merge / split combine as paged_attn_kernel<1>, so results agree to rounding.
+// ------------------------------------------------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void* sd_lds_ptr_t;
+typedef __attribute__((address_space(1))) void* sd_gbl_ptr_t;
+
+template <bool FP8>
+constexpr int sd_step_bytes() { return FP8 ? 8192 : 16384; }  // K + V^T of one 32-token step (two 16-token pages)
+template <bool FP8, int NB>
+constexpr int sd_smem() {
+    constexpr int ring = 4 * NB * sd_step_bytes<FP8>();
+    constexpr int merge = (8 * 16 + 4 * 16 * kOStride) * 4;
+    return ring > merge ? ring : merge;
+}
+
+// One 1 KiB LDS-DMA piece as inline asm (lane l's 16 bytes from its own source address to LDS dst + 16 l).  hipcc
+// cannot see it write LDS, so it does not drain the whole ring (vmcnt(0)) before every ds_read of the step being
+// computed; its completion is counted by the kernel's own sd_vmcnt waits (cdna_hip_programming.md §5.7).
+__device__ __forceinline__ void sd_dma(const void* gsrc, uint32_t lds) {
+    asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(gsrc), "s"(lds) : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void sd_vmcnt() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt((N & 0xF) | (0x7 << 4) | (0xF << 8) | ((N >> 4) << 14));
+}
+
+template <bool FP8, int NB>
+__global__ void __launch_bounds__(256, 1) split_decode_kernel(
+    const uint16_t* __restrict__ q, const void* __restrict__ kcv, const void* __restrict__ vcv,
+    const int32_t* __restrict__ block_table, int bt_stride, const int32_t* __restrict__ ctx_len,
+    uint16_t* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_lse, int hq, int hkv,
+    float scale_log2, float k_scale, float v_scale, const int32_t* __restrict__ gst, int gn, int* __restrict__ cnt) {
+    constexpr int block_size = 16, ROWS = 16;
+    constexpr int SB = sd_step_bytes<FP8>();            // bytes of one step in the ring
+    constexpr int KB = SB / 2;                          // K part (2 pages); V^T part after it
+    constexpr int PK = KB / 1024, PV = KB / 1024;       // LDS-DMA pieces per step: K, V^T
+    constexpr int NP = PK + PV;
+    if (gate_closed(gst, gn)) return;
+    extern __shared__ __attribute__((aligned(1024))) unsigned char sd_smem_raw[];
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r = lane & 15, h4 = lane >> 4;
+    const int G = hq / hkv, h = blockIdx.y, seq = blockIdx.x, nsplit = gridDim.z;
+    const int ctx = ctx_len[seq];
+    unsigned char* ring = sd_smem_raw + w * NB * SB;  // this wave's ring of NB steps
+
+    bf16x8 qf[4];
+    {
+        const bool valid = r < G;
+        const uint16_t* qp = q + ((int64_t)seq * hq + h * G + (valid ? r : 0)) * kD + 8 * h4;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            bf16x8 v = *reinterpret_cast<const bf16x8*>(qp + 32 * c);
+            if (!valid) v = bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+            qf[c] = v;
+        }
+    }
+    sd_vmcnt<0>();  // q landed: the ring's waits below count only this wave's DMA pieces
+    int chunk = (ctx + nsplit - 1) / nsplit;
+    chunk = (chunk + 31) & ~31;
+    const int ks = blockIdx.z * chunk;
+    const int ke = min(ctx, ks + chunk);
+    const int32_t* bt = block_table + (int64_t)seq * bt_stride;
+    const float sl2 = FP8 ? scale_log2 * k_scale : scale_log2;  // fp8: K's cache scale folded into the score scale
+
+    // stage step t0 (wave-uniform) into ring slot j: pages A = t0 / 16, B = A + 1 (past the range: A again, masked)
+    auto stage = [&](int t0, int j) {
+        const uint32_t dl = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(ring + j * SB));
+        const int64_t pa = bt[t0 / block_size];
+        const int64_t pb = t0 + block_size < ke ? bt[t0 / block_size + 1] : pa;
+        if constexpr (!FP8) {
+            // K page: 16 rows x 256 B; piece i of page g = rows 4 i .. +3, lane -> row 4 i + (l >> 4), slot l & 15,
+            // holding the row's chunk slot ^ row (the fragment reads then hit 16 distinct slots)
+#pragma unroll
+            for (int i = 0; i < PK; ++i) {
+                const int g = i >> 2, row = 4 * (i & 3) + (lane >> 4);
+                const int64_t pg = g ? pb : pa;
+                const uint16_t* src = reinterpret_cast<const uint16_t*>(kcv) +
+                                      ((pg * hkv + h) * block_size + row) * kD + 8 * ((lane & 15) ^ row);
+                sd_dma(src, dl + i * 1024);
+            }
+            // V^T page: 128 dims x 32 B contiguous in the cache; piece i of page g = dims 32 (i & 3) .. +31
+#pragma unroll
+            for (int i = 0; i < PV; ++i) {
+                const int g = i >> 2;
+                const int64_t pg = g ? pb : pa;
+                const uint16_t* src = reinterpret_cast<const uint16_t*>(vcv) + (pg * hkv + h) * kD * block_size +
+                                      (i & 3) * 512 + 8 * lane;
+                sd_dma(src, dl + KB + i * 1024);
+            }
+        } else {
+            // fp8 K page: 16 rows x 128 B = 2 pieces (rows 8 i .. +7, lane -> row 8 i + (l >> 3), slot l & 7 holding
+            // chunk slot ^ (row & 7)); V^T page: 128 dims x 16 B = 2 pieces of 64 dims
+#pragma unroll
+            for (int i = 0; i < PK; ++i) {
+                const int g = i >> 1, row = 8 * (i & 1) + (lane >> 3);
+                const int64_t pg = g ? pb : pa;
+                const uint8_t* src = reinterpret_cast<const uint8_t*>(kcv) + ((pg * hkv + h) * block_size + row) * kD +
+                                     16 * ((lane & 7) ^ (row & 7));
+                sd_dma(src, dl + i * 1024);
+            }
+#pragma unroll
+            for (int i = 0; i < PV; ++i) {
+                const int g = i >> 1;
+                const int64_t pg = g ? pb : pa;
+                const uint8_t* src = reinterpret_cast<const uint8_t*>(vcv) + (pg * hkv + h) * kD * block_size +
+                                     (i & 1) * 1024 + 16 * lane;
+                sd_dma(src, dl + KB + i * 1024);
+            }
+        }
+    };
+
+    float m = -1e30f, lsum = 0.f;
+    f32x4 o[8];
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    auto compute = [&](int t0, int j) {
+        const unsigned char* src = ring + j * SB;
+        bf16x8 kf[2][4];
+        bf16x4 vf[2][8];
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            const int row = r;  // page g's token row r
+            if constexpr (!FP8) {
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    kf[g][c] = *reinterpret_cast<const bf16x8*>(src + g * 4096 + row * 256 + (((4 * c + h4) ^ row) << 4));
+#pragma unroll
+                for (int dt = 0; dt < 8; ++dt)
+                    vf[g][dt] = *reinterpret_cast<const bf16x4*>(src + KB + g * 4096 + (dt * 16 + r) * 32 + 8 * h4);
+            } else {
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    // dims 32 c + 8 h4 .. +8 = 16-B chunk 2 c + (h4 >> 1), half h4 & 1
+                    const uint2 v = *reinterpret_cast<const uint2*>(
+                        src + g * 2048 + row * 128 + (((2 * c + (h4 >> 1)) ^ (row & 7)) << 4) + 8 * (h4 & 1));
+                    kf[g][c] = fp8x8_to_bf16x8_raw(v.x, v.y);
+                }
+#pragma unroll
+                for (int dt = 0; dt < 8; ++dt) {
+                    const uint32_t v = *reinterpret_cast<const uint32_t*>(src + KB + g * 2048 + (dt * 16 + r) * 16 +
+                                                                          4 * h4);
+                    const bf16x8 e = fp8x8_to_bf16x8_raw(v, 0u);
+                    vf[g][dt] = bf16x4{e[0], e[1], e[2], e[3]};
+                }
+            }
+        }
+        if (t0 + 32 > ke) {  // partial step: zero V of keys past the end (uniform branch)
+#pragma unroll
+            for (int g = 0; g < 2; ++g)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if (t0 + 16 * g + 4 * h4 + i >= ke)
+#pragma unroll
+                        for (int dt = 0; dt < 8; ++dt) vf[g][dt][i] = (__bf16)0.f;
+        }
+        f32x4 sc[2];
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[g][c], qf[c], acc, 0, 0, 0);
+            sc[g] = acc;
+        }
+        float mx = -INFINITY;
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float v = sc[g][i] * sl2;
+                if (t0 + 16 * g + 4 * h4 + i >= ke) v = -INFINITY;
+                sc[g][i] = v;
+                mx = fmaxf(mx, v);
+            }
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float mnew = fmaxf(m, mx);
+        const float alpha = exp2f(m - mnew);
+        m = mnew;
+        float ps = 0.f;
+        bf16x8 pf;
+#pragma unroll
+        for (int g = 0; g < 2; ++g)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const float p = exp2f(sc[g][i] - mnew);
+                ps += p;
+                pf[4 * g + i] = (__bf16)p;
+            }
+        lsum = lsum * alpha + ps;
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) {
+            o[dt] *= alpha;
+            const bf16x8 va = __builtin_shufflevector(vf[0][dt], vf[1][dt], 0, 1, 2, 3, 4, 5, 6, 7);
+            o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(va, pf, o[dt], 0, 0, 0);
+        }
+    };
+
+    // the wave's steps: t0 = ks + 32 w + 128 i; NB of them in flight (ring slot i % NB)
+    const int t_first = ks + 32 * w;
+    const int nsteps = t_first < ke ? (ke - t_first + 127) / 128 : 0;
+#pragma unroll
+    for (int i = 0; i < NB - 1; ++i)
+        if (i < nsteps) stage(t_first + 128 * i, i);
+    for (int i = 0; i < nsteps; ++i) {
+        const int ahead = i + NB - 1;
+        const bool more = ahead < nsteps;  // wave-uniform
+        if (more) stage(t_first + 128 * ahead, ahead % NB);
+        // step i landed: the pieces issued after it (up to NB - 1 steps) may stay in flight
+        const int newer = min(nsteps - 1 - i, NB - 1);
+        if (newer >= 2) sd_vmcnt<2 * NP>();
+        else if (newer == 1) sd_vmcnt<NP>();
+        else sd_vmcnt<0>();
+        compute(t_first + 128 * i, i % NB);
+    }
+    sd_vmcnt<0>();
+    __syncthreads();  // the ring is reused as the merge buffer below
+
+    float* sm = reinterpret_cast<float*>(sd_smem_raw);
+    float* sl = sm + 4 * ROWS;
+    float* so = sl + 4 * ROWS;
+    const float oscale = FP8 ? v_scale : 1.f;  // fp8: V's cache scale applied once to the merged output
+    {
+        float lt = lsum;
+        lt += __shfl_xor(lt, 16, 64);
+        lt += __shfl_xor(lt, 32, 64);
+        if (h4 == 0) {
+            sm[w * ROWS + r] = m;
+            sl[w * ROWS + r] = lt;
+        }
+        float* orow = so + (w * ROWS + r) * kOStride;
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) *reinterpret_cast<f32x4*>(orow + dt * 16 + 4 * h4) = o[dt];
+    }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < ROWS * 16; idx += 256) {
+        const int row = idx >> 4, c8 = idx & 15;
+        if (row >= G) continue;
+        const int hd = h * G + row;
+        float M = -1e30f;
+#pragma unroll
+        for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, sm[ww * ROWS + row]);
+        float L = 0.f, acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+        for (int ww = 0; ww < 4; ++ww) {
+            const float f = exp2f(sm[ww * ROWS + row] - M);
+            L += sl[ww * ROWS + row] * f;
+            const float* orow = so + (ww * ROWS + row) * kOStride + c8 * 8;
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) acc[jj] += orow[jj] * f;
+        }
+        const float inv = L > 0.f ? oscale / L : 0.f;
+        if (nsplit == 1) {
+            u16x8 ov;
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) ov[jj] = f2bf(acc[jj] * inv);
+            *reinterpret_cast<u16x8*>(out + ((int64_t)seq * hq + hd) * kD + c8 * 8) = ov;
+        } else {
+            const int64_t prow = (((int64_t)blockIdx.z * gridDim.x + seq) * hkv + h) * ROWS + row;
+            float* po = part_o + prow * kD + c8 * 8;
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) po[jj] = acc[jj] * inv;
+            if (c8 == 0) part_lse[prow] = L > 0.f ? M + __log2f(L) : -INFINITY;
+        }
+    }
+    if (nsplit == 1 || cnt == nullptr) return;
+    int* flag = reinterpret_cast<int*>(sm);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        int* c = cnt + (int64_t)seq * hkv + h;
+        const int old = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = old == nsplit - 1;
+        if (last) {
+            __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        flag[0] = last;
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+    combine_tile<1>(part_o, part_lse, out, seq, h, 0, seq, 1, hq, hkv, nsplit, gridDim.x);
+}
+
 template <int NQT>
 __global__ void __launch_bounds__(256) paged_attn_combine_kernel(
     const float* __restrict__ part_o, const float* __restrict__ part_lse, const int32_t* __restrict__ q_start,
@@ -957,6 +1256,32 @@ void launch_paged_attn(const uint16_t* q, const void* kc, const void* vc, const 
     }
 legacy:
     const dim3 grid(ntiles, hkv, nsplit), block(256);
+    if (tiles == nullptr && nqt == 1 && nsplit > 1 && hq / hkv <= 16 && block_size == 16 && knob("split_lds", 1)) {
+        // long-context decode: the LDS-staged split kernel (lane-linear LDS-DMA, NB steps in flight per wave)
+        int* cnt = nsplit <= knob("inkernel_combine_max_split", 4) ? tickets_for((int64_t)ntiles * hkv) : nullptr;
+        int nb = knob("split_lds_nb", 0);  // ring depth (steps in flight per wave); <= 0: the default
+        if (nb <= 0) nb = fp8 ? 3 : 2;
+#define SD_LAUNCH(F, NB)                                                                                          \
+    {                                                                                                           \
+        constexpr int shm = sd_smem<F, NB>();                                                                    \
+        auto kern = split_decode_kernel<F, NB>;                                                                  \
+        static bool attr = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,     \
+                                               shm) == hipSuccess;                                              \
+        (void)attr;                                                                                             \
+        hipLaunchKernelGGL(kern, grid, block, shm, st, q, kc, vc, block_table, bt_stride, ctx_len, out, part_o,   \
+                           part_lse, hq, hkv, scale_log2, k_scale, v_scale, CHRONOS_GATE, cnt);                 \
+    }
+        if (fp8) {
+            if (nb >= 4) SD_LAUNCH(true, 4) else if (nb == 3) SD_LAUNCH(true, 3) else SD_LAUNCH(true, 2)
+        } else {
+            if (nb >= 2) SD_LAUNCH(false, 2) else SD_LAUNCH(false, 1)
+        }
+#undef SD_LAUNCH
+        if (cnt == nullptr)
+            hipLaunchKernelGGL(paged_attn_combine_kernel<1>, dim3(ntiles, hkv), block, 0, st, part_o, part_lse,
+                               q_start, tiles, out, hq, hkv, nsplit, ntiles, CHRONOS_GATE);
+        return;
+    }
     // in-launch combine (last split merges) only for a few splits: with many splits the per-workgroup agent-scope
     // release + ticket costs more than the separate combine launch it saves (128k single-sequence decode, 64 splits:
     // 147 vs 132 us per layer; profiles/r2_attn_split_combine.jsonl)

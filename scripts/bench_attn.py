@@ -52,8 +52,9 @@ def main():
         cases = ((1024, 128, False), (1024, 144, False))
     if os.environ.get("ATTN_CASES") == "long":  # split-K decode over long contexts (the 128k config's decode)
         cases = ((1, 131072, False), (1, 131072, True), (4, 32768, False), (16, 8192, False), (64, 1024, False))
-        variants = {"split": dict(split_pf=0, attn_inkernel_combine=1), "split_pf": dict(split_pf=1, attn_inkernel_combine=1),
-                    "split_pf_sepcomb": dict(split_pf=1, attn_inkernel_combine=0)}
+        variants = {"split_pf": dict(split_lds=0, split_pf=1, attn_inkernel_combine=1),
+                    "lds_nb1": dict(split_lds=1, split_lds_nb=1), "lds_nb2": dict(split_lds=1, split_lds_nb=2),
+                    "lds_nb3": dict(split_lds=1, split_lds_nb=3), "lds_nb4": dict(split_lds=1, split_lds_nb=4)}
     for B, ctx, fp8 in cases:
         hq, hkv, bs = 32, 8, 16
         nbs = (ctx + bs - 1) // bs
@@ -79,8 +80,12 @@ def main():
         res = {}
         outs = {}
         runs = [(name, kn, ns) for name, kn in variants.items()]
-        if os.environ.get("ATTN_NSPLITS"):  # the split count itself (default kernel knobs)
-            runs = [(f"nsplit{n}", {}, int(n)) for n in os.environ["ATTN_NSPLITS"].split(",")]
+        if os.environ.get("ATTN_NSPLITS"):  # the split count itself (default kernel knobs, or ATTN_KNOBS sets)
+            kn_sets = [dict(kv.split("=") for kv in ks.split("+")) if ks else {}
+                       for ks in os.environ.get("ATTN_KNOBS", "").split(",")]
+            runs = [(f"nsplit{n}" + ("_" + "_".join(f"{a}{b}" for a, b in kd.items()) if kd else ""),
+                     {a: int(b) for a, b in kd.items()}, int(n))
+                    for n in os.environ["ATTN_NSPLITS"].split(",") for kd in kn_sets]
         for name, kn, nsp in runs:
             for kk, vv in kn.items():
                 C.set_knob(kk, vv)
@@ -100,6 +105,8 @@ def main():
     C.set_knob("decode_occ3", 1)
     C.set_knob("split_pf", 1)
     C.set_knob("attn_inkernel_combine", 1)
+    C.set_knob("split_lds", 1)
+    C.set_knob("split_lds_nb", 0)
     if a.out:
         with open(a.out, "w") as fh:
             json.dump(out, fh, indent=1)

@@ -1,0 +1,73 @@
+"""LDS-staged split-K decode attention (csrc/kernels/attention.hip split_decode_kernel) against the
+fp32 reference, bf16 and fp8-e4m3 KV, every ring depth, long and ragged contexts (splits with no keys, partial last
+steps, contexts not a multiple of the 32-token step), the in-launch combine and the separate combine kernel."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib():
+    from chronos import ops
+
+    ops.load()
+    yield
+    torch.ops.chronos.set_knob("split_lds", 1)
+    torch.ops.chronos.set_knob("split_lds_nb", -1)
+    torch.ops.chronos.set_knob("attn_inkernel_combine", 1)
+
+
+def _case(ctx, hq, hkv, fp8, seed):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    bs = 16
+    B = len(ctx)
+    nbs = [(c + bs - 1) // bs for c in ctx]
+    nb = sum(nbs) + 1
+    perm = (torch.randperm(nb - 1, generator=torch.Generator().manual_seed(seed)) + 1).tolist()
+    bt = torch.zeros(B, max(nbs), dtype=torch.int32)
+    o = 0
+    for b, n in enumerate(nbs):
+        bt[b, :n] = torch.tensor(perm[o:o + n])
+        o += n
+    if fp8:
+        from chronos.ops import reference as ref
+
+        k = ref.to_fp8_bytes(torch.randn(nb, hkv, bs, 128, device=DEV, generator=g) * 1.5, 1.0 / 0.5)
+        v = ref.to_fp8_bytes(torch.randn(nb, hkv, 128, bs, device=DEV, generator=g), 1.0 / 0.25)
+    else:
+        k = (torch.randn(nb, hkv, bs, 128, device=DEV, generator=g) * 0.7).to(torch.bfloat16)
+        v = torch.randn(nb, hkv, 128, bs, device=DEV, generator=g).to(torch.bfloat16)
+    q = (torch.randn(B, hq, 128, device=DEV, generator=g)).to(torch.bfloat16)
+    qs = torch.arange(B + 1, dtype=torch.int32, device=DEV)
+    return q, k, v, bt.to(DEV), qs, torch.tensor(ctx, dtype=torch.int32, device=DEV)
+
+
+@pytest.mark.parametrize("fp8,nb", [(False, 1), (False, 2), (True, 2), (True, 3), (True, 4)])
+@pytest.mark.parametrize("ctx,nsplit", [([33000], 32), ([8191, 100, 4097], 16), ([700, 33, 1, 480], 4),
+                                        ([131072], 32)])
+def test_split_lds_matches_reference(fp8, nb, ctx, nsplit):
+    from chronos import ops
+    from chronos.ops import reference as ref
+
+    if ctx == [131072] and nb not in (2, 3):
+        pytest.skip("the 128k case once per dtype")
+    hq, hkv = 32, 8
+    q, k, v, bt, qs, cl = _case(ctx, hq, hkv, fp8, seed=sum(ctx) + nb)
+    ks, vs = (0.5, 0.25) if fp8 else (1.0, 1.0)
+    torch.ops.chronos.set_knob("split_lds_nb", nb)
+    outs = {}
+    for lds in (1, 0):
+        torch.ops.chronos.set_knob("split_lds", lds)
+        for comb in (1, 0):
+            torch.ops.chronos.set_knob("attn_inkernel_combine", comb)
+            outs[(lds, comb)] = ops.paged_attention(q, k, v, bt, qs, cl, None, len(ctx), 1, nsplit, None, ks, vs).float()
+    torch.ops.chronos.set_knob("split_lds", 1)
+    torch.ops.chronos.set_knob("attn_inkernel_combine", 1)
+    want = ref.paged_attention(q, k, v, bt, qs, cl, None, len(ctx), 1, nsplit, None, ks, vs).float()
+    tol = 2e-2 * want.abs().max().item()
+    for key, o in outs.items():
+        assert (o - want).abs().max().item() <= tol, (key, (o - want).abs().max().item(), tol)
+    # in-launch combine == separate combine kernel (same merge code)
+    assert torch.equal(outs[(1, 1)], outs[(1, 0)])
