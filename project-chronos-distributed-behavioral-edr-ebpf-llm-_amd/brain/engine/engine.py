@@ -98,6 +98,9 @@ class EngineConfig:
     tp_overlap: bool = True        # TP prefill: two micro-batches, each one's RCCL all-reduces overlap the other's compute
     tp_overlap_min_tokens: int = 1024
     tp_sequence_parallel: bool = False  # TP prefill: reduce-scatter / all-gather around the norms instead of all-reduce
+    # TP decode: batches of at least this many rows run as two halves whose fused IPC all-reduce + norm launches
+    # overlap the other half's compute on a second HIP stream (LlamaModel._forward_dec_overlap; 0 = off)
+    tp_decode_overlap: int = 0
     decode_gate: bool = True       # small buckets: kernels of steps after the last live row finished return at once
     cp_min_tokens: int = 4096      # context parallel (Engine(cp=...)): prefill chunks at least this long are split
     cp_mode: str = "allgather"     # "allgather" (zigzag token pieces) or "ulysses" (head-sharded attention)
@@ -232,6 +235,7 @@ class Engine:
                                           max_position=cfg.max_model_len + 16, weight_dtype=cfg.weight_dtype)
         self.load_seconds = time.perf_counter() - t0
         self.model.sequence_parallel = cfg.tp_sequence_parallel and self.tp.world > 1
+        self.model.decode_overlap_rows = cfg.tp_decode_overlap if self.tp.world > 1 else 0
         mc = self.model.cfg
         self.bank = GrammarBank(self.tok.token_bytes_list(), self.tok.stop_ids, mc.vocab_size, cfg.grammar_capacity,
                                 self.device, max_string=cfg.max_string,

@@ -562,6 +562,11 @@ class LlamaModel:
         self.scale = 1.0 / math.sqrt(cfg.head_dim)
         # Megatron-style sequence parallelism for TP prefill (set by the engine, EngineConfig.tp_sequence_parallel)
         self.sequence_parallel = False
+        # TP decode comm/compute overlap (set by the engine, EngineConfig.tp_decode_overlap): decode batches of at least
+        # this many rows run as two row halves whose fused IPC all-reduce + residual + RMSNorm launches go to a second
+        # HIP stream, each overlapping the other half's attention / MLP (0 = off)
+        self.decode_overlap_rows = 0
+        self._comm = None
 
     # ---- one micro-batch's pieces of a layer (bf16: x is a tensor; W8A8: x is (e4m3 bytes, row scales)) ----------
     def _norm(self, h, st: dict, w: torch.Tensor, first: bool = False, reduce: bool = False):
@@ -676,6 +681,74 @@ class LlamaModel:
         logits = tp.all_gather_last(ops.linear(x, w.lm_head))
         return logits if logits.dtype == logits_dtype else logits.to(logits_dtype)
 
+    def _decode_halves(self, sb: StepBatch) -> list:
+        """Two decode-mode StepBatches over rows [0, h) and [h, n) of a decode batch (views of the slot state: decode
+        rows are seq i = token i, q_start / tok_seq / last_idx are aranges, so each half re-uses their prefix)."""
+        n = sb.ntiles
+        h = (n + 1) // 2
+        halves = []
+        for a, b in ((0, h), (h, n)):
+            m = b - a
+            halves.append(StepBatch(sb.ids[a:b], sb.pos[a:b], sb.tok_seq[:m], sb.block_table[a:b], sb.q_start[:m + 1],
+                                    sb.ctx_len[a:b], sb.last_idx[:m], None, m, sb.nqt, sb.nsplit))
+        return halves
+
+    def _forward_dec_overlap(self, sb: StepBatch, kv: KVCache, logits_dtype) -> torch.Tensor:
+        """TP decode with comm/compute overlap: the batch's two row halves A, B run
+        layer by layer on the compute stream while every row-parallel projection's all-reduce — the fused IPC one-shot
+        + residual add + RMSNorm — runs on a second stream (``self._comm``), ordered by events:
+
+            compute: attn(A) | attn(B) | wait ARo(A) mlp(A) | wait ARo(B) mlp(B) | wait ARd(A) attn'(A) ...
+            comm:            ARo(A)   ARo(B)               ARd(A)             ARd(B)
+
+        so half A's all-reduce hides behind half B's compute and vice versa.  All all-reduces share ONE stream, issued
+        in the same order on every rank (the IPC kernel's epoch lives on the device: one sequence per rank).  Both
+        streams are captured into the decode hipGraph (the side stream forks from and joins the compute stream through
+        events).  Allocator safety without record_stream (which graph capture does not like): every comm-stream launch
+        first waits for the compute stream's current tail, and a compute-stream tensor the comm stream reads (the
+        partial sums) stays referenced until the compute stream has waited for that launch."""
+        cfg, w, tp = self.cfg, self.w, self.tp
+        main = torch.cuda.current_stream(self.device)
+        if self._comm is None:
+            self._comm = torch.cuda.Stream(self.device)
+        comm = self._comm
+        eps = cfg.rms_eps
+
+        def ar_norm(st, hpart, wn):
+            ev = torch.cuda.Event()
+            ev.record(main)
+            comm.wait_event(ev)
+            with torch.cuda.stream(comm):
+                x = tp.all_reduce_add_rmsnorm(hpart, st["resid"], wn, eps)
+            done = torch.cuda.Event()
+            done.record(comm)
+            return x, done, hpart
+
+        states = []
+        for p in self._decode_halves(sb):
+            h = tp.all_reduce(ops.embedding(p.ids, w.embed, w.vocab_start))
+            T = p.ids.numel()
+            st = dict(sb=p, T=T, resid=h, q_buf=torch.empty(T, self.hq, cfg.head_dim, device=h.device, dtype=h.dtype))
+            st["x"] = self._norm(h, st, w.layers[0].attn_norm, first=True)
+            states.append(st)
+        L = len(w.layers)
+        for li, lw in enumerate(w.layers):
+            pend = [ar_norm(st, self._attn(li, lw, st, kv), lw.mlp_norm) for st in states]
+            pend2 = []
+            for st, (x, done, _) in zip(states, pend):
+                main.wait_event(done)
+                st["x"] = x
+                nxt = w.layers[li + 1].attn_norm if li + 1 < L else w.norm
+                pend2.append(ar_norm(st, self._mlp(lw, st), nxt))
+            del pend
+            for st, (x, done, _) in zip(states, pend2):
+                main.wait_event(done)
+                st["x"] = x
+            del pend2
+        logits = ops.linear(torch.cat([st["x"] for st in states]), w.lm_head)
+        logits = tp.all_gather_last(logits)
+        return logits if logits.dtype == logits_dtype else logits.to(logits_dtype)
+
     def forward(self, sb: StepBatch, kv: KVCache, logits_dtype=torch.bfloat16) -> torch.Tensor:
         """Returns logits [B, V] for the token at sb.last_idx of every sequence (full vocab on every TP rank).
 
@@ -689,6 +762,10 @@ class LlamaModel:
         if (tp.world > 1 and sb.tiles is not None and self.sequence_parallel and not w.fp8 and sb.cp is None
                 and sb.dec is None):
             return self._forward_sp(sb, kv, logits_dtype)
+        if (0 < self.decode_overlap_rows <= sb.ntiles and sb.tiles is None and sb.dec is None and sb.cp is None
+                and tp.world > 1 and tp.fast_allreduce_norm is not None and not w.fp8 and _FUSE_AR_NORM
+                and self.device.type == "cuda"):
+            return self._forward_dec_overlap(sb, kv, logits_dtype)
         parts = sb.parts if (sb.parts and tp.world > 1) else [sb]
         overlap = len(parts) > 1
         # TP, one part: the all-reduce after o_proj / down_proj is fused with the residual add + RMSNorm that follows
