@@ -33,6 +33,54 @@ __device__ __forceinline__ void combine_tile(const float* __restrict__ part_o, c
                                              int qlen, int hq, int hkv, int nsplit, int ntiles) {
     constexpr int ROWS = NQT * 16;
     const int G = hq / hkv;
+    if (NQT == 1 && qlen == 1 && rel0 == 0 && G <= 16) {
+        // decode (one query row per sequence): only G of the 16 rows are live, so the G x 16 (row, 8-column group)
+        // items take P adjacent lanes each, the lanes split the splits between them and merge through shuffles —
+        // P times fewer dependent global-load rounds than one lane walking all nsplit partials (128k decode: 32
+        // splits x 8 kv heads, 17.5 -> a few us per layer)
+        const int items = G * 16;
+        const int P = items <= 16 ? 16 : items <= 32 ? 8 : items <= 64 ? 4 : items <= 128 ? 2 : 1;
+        const int item = threadIdx.x / P, sub = threadIdx.x % P;
+        const bool live = item < items;
+        const int row = live ? item >> 4 : 0, c8 = item & 15;
+        const int64_t base = ((int64_t)tile * hkv + h) * ROWS + row;
+        const int64_t sstride = (int64_t)ntiles * hkv * ROWS;
+        float M = -INFINITY;
+        if (live)
+            for (int s = sub; s < nsplit; s += P) M = fmaxf(M, part_lse[base + s * sstride]);
+        for (int o = 1; o < P; o <<= 1) M = fmaxf(M, __shfl_xor(M, o));
+        float L = 0.f, acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (live && M > -INFINITY) {
+#pragma unroll 4
+            for (int s = sub; s < nsplit; s += P) {
+                const int64_t prow = base + s * sstride;
+                const float l = part_lse[prow];
+                const f32x4 a = *reinterpret_cast<const f32x4*>(part_o + prow * kD + c8 * 8);
+                const f32x4 b = *reinterpret_cast<const f32x4*>(part_o + prow * kD + c8 * 8 + 4);
+                const bool on = l > -INFINITY;  // an empty split's partial row may be stale: never multiply it
+                const float f = on ? exp2f(l - M) : 0.f;
+                L += f;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    acc[j] += on ? a[j] * f : 0.f;
+                    acc[4 + j] += on ? b[j] * f : 0.f;
+                }
+            }
+        }
+        for (int o = 1; o < P; o <<= 1) {
+            L += __shfl_xor(L, o);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[j] += __shfl_xor(acc[j], o);
+        }
+        if (live && sub == 0) {
+            const float inv = L > 0.f ? 1.f / L : 0.f;
+            u16x8 ov;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) ov[j] = f2bf(acc[j] * inv);
+            *reinterpret_cast<u16x8*>(out + ((int64_t)qbase * hq + h * G + row) * kD + c8 * 8) = ov;
+        }
+        return;
+    }
     for (int idx = threadIdx.x; idx < ROWS * 16; idx += 256) {
         const int row = idx >> 4, c8 = idx & 15;
         const int tr = rel0 + row / G, hd = h * G + row % G;
@@ -1258,9 +1306,9 @@ legacy:
     const dim3 grid(ntiles, hkv, nsplit), block(256);
     if (tiles == nullptr && nqt == 1 && nsplit > 1 && hq / hkv <= 16 && block_size == 16 && knob("split_lds", 1)) {
         // long-context decode: the LDS-staged split kernel (lane-linear LDS-DMA, NB steps in flight per wave)
-        int* cnt = nsplit <= knob("inkernel_combine_max_split", 4) ? tickets_for((int64_t)ntiles * hkv) : nullptr;
+        int* cnt = nsplit <= knob("sd_inkernel_max_split", 4) ? tickets_for((int64_t)ntiles * hkv) : nullptr;
         int nb = knob("split_lds_nb", 0);  // ring depth (steps in flight per wave); <= 0: the default
-        if (nb <= 0) nb = fp8 ? 3 : 2;
+        if (nb <= 0) nb = 2;  // (r5 sweep after the parallel combine: fp8 nb2 52.5 us vs nb3 54.7 at 128k)
 #define SD_LAUNCH(F, NB)                                                                                          \
     {                                                                                                           \
         constexpr int shm = sd_smem<F, NB>();                                                                    \

@@ -54,7 +54,9 @@ def main():
         cases = ((1, 131072, False), (1, 131072, True), (4, 32768, False), (16, 8192, False), (64, 1024, False))
         variants = {"split_pf": dict(split_lds=0, split_pf=1, attn_inkernel_combine=1),
                     "lds_nb1": dict(split_lds=1, split_lds_nb=1), "lds_nb2": dict(split_lds=1, split_lds_nb=2),
-                    "lds_nb3": dict(split_lds=1, split_lds_nb=3), "lds_nb4": dict(split_lds=1, split_lds_nb=4)}
+                    "lds_nb3": dict(split_lds=1, split_lds_nb=3), "lds_nb4": dict(split_lds=1, split_lds_nb=4),
+                    "lds_inlaunch": dict(split_lds=1, split_lds_nb=0, sd_inkernel_max_split=1024),
+                    "lds_sepcomb": dict(split_lds=1, split_lds_nb=0, sd_inkernel_max_split=4)}
     for B, ctx, fp8 in cases:
         hq, hkv, bs = 32, 8, 16
         nbs = (ctx + bs - 1) // bs
@@ -107,6 +109,7 @@ def main():
     C.set_knob("attn_inkernel_combine", 1)
     C.set_knob("split_lds", 1)
     C.set_knob("split_lds_nb", 0)
+    C.set_knob("sd_inkernel_max_split", 4)
     if a.out:
         with open(a.out, "w") as fh:
             json.dump(out, fh, indent=1)

@@ -17,6 +17,7 @@ def _lib():
     torch.ops.chronos.set_knob("split_lds", 1)
     torch.ops.chronos.set_knob("split_lds_nb", -1)
     torch.ops.chronos.set_knob("attn_inkernel_combine", 1)
+    torch.ops.chronos.set_knob("sd_inkernel_max_split", 4)
 
 
 def _case(ctx, hq, hkv, fp8, seed):
@@ -62,9 +63,11 @@ def test_split_lds_matches_reference(fp8, nb, ctx, nsplit):
         torch.ops.chronos.set_knob("split_lds", lds)
         for comb in (1, 0):
             torch.ops.chronos.set_knob("attn_inkernel_combine", comb)
+            torch.ops.chronos.set_knob("sd_inkernel_max_split", 1024 if comb else 4)
             outs[(lds, comb)] = ops.paged_attention(q, k, v, bt, qs, cl, None, len(ctx), 1, nsplit, None, ks, vs).float()
     torch.ops.chronos.set_knob("split_lds", 1)
     torch.ops.chronos.set_knob("attn_inkernel_combine", 1)
+    torch.ops.chronos.set_knob("sd_inkernel_max_split", 4)
     want = ref.paged_attention(q, k, v, bt, qs, cl, None, len(ctx), 1, nsplit, None, ks, vs).float()
     tol = 2e-2 * want.abs().max().item()
     for key, o in outs.items():
