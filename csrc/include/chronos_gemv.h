@@ -18,6 +18,7 @@ struct GemvNorm {
     const uint16_t* rin;   // producer: residual in [M, N]
     uint16_t* rout;        // producer: residual out [M, N]
     float* part_out;       // producer: partials [M, gridDim.x]
+    const float* wscale;   // fp8-e4m3 weights (W8A16): per-output-row scale [N]; nullptr = bf16 weights
 };
 
 struct GemvRope {
@@ -35,11 +36,12 @@ struct GemvRope {
 
 // consumer: x = s (the residual stream a kResid producer wrote), nrm->part/nparts/w/eps set; rope != nullptr: QKV with
 // the RoPE + paged-KV epilogue (y unused).  nrm == nullptr: plain input.
+// wscale != nullptr: W is fp8-e4m3 bytes [N, K] with per-row scales (W8A16: bf16 activations, K % 1024 == 0, M <= 2)
 void launch_gemv_ex(const uint16_t* x, int M, int K, const uint16_t* W, int N, uint16_t* y, bool swiglu,
-                    const GemvNorm* nrm, const GemvRope* rope, bool fp8, hipStream_t st);
+                    const GemvNorm* nrm, const GemvRope* rope, bool fp8, hipStream_t st, const float* wscale = nullptr);
 // producer: rout = bf16(bf16(x @ W^T) + rin), part_out[m, wg] = per-workgroup sum of rout^2; returns nparts
 int launch_gemv_resid(const uint16_t* x, int M, int K, const uint16_t* W, int N, const uint16_t* rin, uint16_t* rout,
-                      float* part_out, hipStream_t st);
+                      float* part_out, hipStream_t st, const float* wscale = nullptr);
 int gemv_resid_parts(int M, int N);
 
 }  // namespace chronos

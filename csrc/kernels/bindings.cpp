@@ -121,6 +121,21 @@ inline void chk_i32(const Tensor& t, const char* n) {
     CHK(t.scalar_type() == at::kInt, std::string(n) + " must be int32");
 }
 
+// Decode GEMV weights: bf16 [N, K], or (ws given) fp8-e4m3 bytes [N, K] with per-row f32 scales [N] (W8A16: the
+// fp8-weight model's decode step keeps bf16 activations; csrc/kernels/gemv.hip WQ).  Returns the scale pointer.
+inline const float* chk_gemv_w(const Tensor& w, const c10::optional<Tensor>& ws, int64_t K, int64_t M) {
+    chk_gpu(w, "w");
+    if (!ws.has_value()) {
+        CHK(w.scalar_type() == at::kBFloat16, "w must be bfloat16 (or uint8 e4m3 with ws)");
+        return nullptr;
+    }
+    chk_gpu(*ws, "ws");
+    CHK(w.scalar_type() == at::kByte, "w must be uint8 (e4m3 bytes) when ws is given");
+    CHK(ws->scalar_type() == at::kFloat && ws->numel() == w.size(0), "ws must be [N] f32");
+    CHK(K % 1024 == 0 && M <= 2, "fp8-weight GEMV: K % 1024 == 0, M <= 2");
+    return ws->data_ptr<float>();
+}
+
 // KV caches are bf16 or fp8-e4m3 stored as uint8 (OCP e4m3fn bytes; dequantised with a per-layer scale)
 inline bool chk_kv(const Tensor& k, const Tensor& v) {
     chk_gpu(k, "k_cache");
@@ -368,17 +383,21 @@ void constrained_sample(const Tensor& logits, const c10::optional<Tensor>& row_o
 }
 
 // y = x @ w.T for M <= 8 rows (decode); swiglu: w = [gate; up] -> y = silu(x@gate.T) * (x@up.T)
-Tensor gemv(const Tensor& x, const Tensor& w, bool swiglu) {
+Tensor gemv(const Tensor& x, const Tensor& w, bool swiglu, const c10::optional<Tensor>& ws) {
     chk_bf16(x, "x");
-    chk_bf16(w, "w");
     const int64_t K = x.size(-1), M = x.numel() / K, N = w.size(0);
+    const float* wsc = chk_gemv_w(w, ws, K, M);
     CHK(w.dim() == 2 && w.size(1) == K, "gemv: w must be [N, K]");
     CHK(M >= 1 && M <= 8, "gemv: 1 <= M <= 8");
     CHK(K % 512 == 0, "gemv: K % 512 == 0");
     CHK(N % 16 == 0, "gemv: N % 16 == 0");
     c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
     auto y = at::empty({M, swiglu ? N / 2 : N}, x.options());
-    chronos::launch_gemv(bf(x), (int)M, (int)K, bf(w), (int)N, bfm(y), swiglu, cur_stream());
+    if (wsc)
+        chronos::launch_gemv_ex(bf(x), (int)M, (int)K, bf(w), (int)N, bfm(y), swiglu, nullptr, nullptr, false,
+                                cur_stream(), wsc);
+    else
+        chronos::launch_gemv(bf(x), (int)M, (int)K, bf(w), (int)N, bfm(y), swiglu, cur_stream());
     return y;
 }
 
@@ -398,12 +417,13 @@ void set_decode_gate(const c10::optional<Tensor>& state, int64_t n) {
 
 // Decode producer (O / down projection at TP=1, M <= 2): resid_out = bf16(bf16(x @ w.T) + resid_in); returns the
 // per-workgroup sums of resid_out^2 [M, P] f32 that the consuming GEMV's norm prologue reduces (chronos_gemv.h).
-Tensor gemv_resid(const Tensor& x, const Tensor& w, const Tensor& resid_in, const Tensor& resid_out) {
+Tensor gemv_resid(const Tensor& x, const Tensor& w, const Tensor& resid_in, const Tensor& resid_out,
+                  const c10::optional<Tensor>& ws) {
     chk_bf16(x, "x");
-    chk_bf16(w, "w");
     chk_bf16(resid_in, "resid_in");
     chk_bf16(resid_out, "resid_out");
     const int64_t K = x.size(-1), M = x.numel() / K, N = w.size(0);
+    const float* wsc = chk_gemv_w(w, ws, K, M);
     CHK(w.dim() == 2 && w.size(1) == K, "gemv_resid: w must be [N, K]");
     CHK(M >= 1 && M <= 2 && K % 512 == 0 && N % 16 == 0, "gemv_resid: M <= 2, K % 512, N % 16");
     CHK(resid_in.numel() == M * N && resid_out.numel() == M * N, "gemv_resid: residuals must be [M, N]");
@@ -411,7 +431,7 @@ Tensor gemv_resid(const Tensor& x, const Tensor& w, const Tensor& resid_in, cons
     c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
     auto part = at::empty({M, chronos::gemv_resid_parts((int)M, (int)N)}, x.options().dtype(at::kFloat));
     chronos::launch_gemv_resid(bf(x), (int)M, (int)K, bf(w), (int)N, bf(resid_in), bfm(resid_out),
-                               part.data_ptr<float>(), cur_stream());
+                               part.data_ptr<float>(), cur_stream(), wsc);
     return part;
 }
 
@@ -431,16 +451,18 @@ inline chronos::GemvNorm normp_args(const Tensor& s, const Tensor& part, double 
 // Decode consumer: y = rmsnorm(s) @ w.T for a projection w whose norm weight is folded in (models/llama.py
 // fold_norm), the norm's sum of squares taken from a gemv_resid producer's partials (swiglu: gate/up pair ->
 // silu(g) * u).  s: [M, K], M <= 2.
-Tensor gemv_normp(const Tensor& s, const Tensor& part, double eps, const Tensor& w, bool swiglu) {
+Tensor gemv_normp(const Tensor& s, const Tensor& part, double eps, const Tensor& w, bool swiglu,
+                  const c10::optional<Tensor>& ws) {
     chk_bf16(s, "s");
-    chk_bf16(w, "w");
     const int64_t K = s.size(-1), M = s.numel() / K, N = w.size(0);
+    const float* wsc = chk_gemv_w(w, ws, K, M);
     CHK(w.dim() == 2 && w.size(1) == K, "gemv_normp: w must be [N, K]");
     CHK(M >= 1 && M <= 2 && K % 512 == 0 && N % 16 == 0, "gemv_normp: M <= 2, K % 512, N % 16");
     const chronos::GemvNorm n = normp_args(s, part, eps, M);
     c10::hip::HIPGuardMasqueradingAsCUDA g(s.device());
     auto y = at::empty({M, swiglu ? N / 2 : N}, s.options());
-    chronos::launch_gemv_ex(bf(s), (int)M, (int)K, bf(w), (int)N, bfm(y), swiglu, &n, nullptr, false, cur_stream());
+    chronos::launch_gemv_ex(bf(s), (int)M, (int)K, bf(w), (int)N, bfm(y), swiglu, &n, nullptr, false, cur_stream(),
+                            wsc);
     return y;
 }
 
@@ -450,9 +472,8 @@ Tensor gemv_normp(const Tensor& s, const Tensor& part, double eps, const Tensor&
 void qkv_rope(const Tensor& x, const c10::optional<Tensor>& part, double eps,
               const Tensor& w, const Tensor& pos, const Tensor& tok_seq, const Tensor& block_table,
               const Tensor& cos_sin, const Tensor& q_out, const Tensor& k_cache, const Tensor& v_cache, int64_t hq,
-              int64_t hkv, double k_scale, double v_scale) {
+              int64_t hkv, double k_scale, double v_scale, const c10::optional<Tensor>& ws) {
     chk_bf16(x, "x");
-    chk_bf16(w, "w");
     chk_i32(pos, "pos");
     chk_i32(tok_seq, "tok_seq");
     chk_i32(block_table, "block_table");
@@ -461,6 +482,7 @@ void qkv_rope(const Tensor& x, const c10::optional<Tensor>& part, double eps,
     chk_bf16(q_out, "q_out");
     const bool fp8 = chk_kv(k_cache, v_cache);
     const int64_t K = x.size(-1), M = x.numel() / K, N = w.size(0);
+    const float* wsc = chk_gemv_w(w, ws, K, M);
     CHK(M >= 1 && M <= 2 && K % 512 == 0, "qkv_rope: M <= 2, K % 512 == 0");
     CHK(w.dim() == 2 && w.size(1) == K && N == (hq + 2 * hkv) * 128, "w must be [(hq+2hkv)*128, K]");
     CHK(pos.numel() >= M && tok_seq.numel() >= M && q_out.numel() >= M * hq * 128, "pos/tok_seq/q_out too small");
@@ -475,7 +497,7 @@ void qkv_rope(const Tensor& x, const c10::optional<Tensor>& part, double eps,
                          bfm(q_out), k_cache.data_ptr(), v_cache.data_ptr(), (int)hq, (int)hkv, (int)k_cache.size(2),
                          (float)(1.0 / k_scale), (float)(1.0 / v_scale)};
     chronos::launch_gemv_ex(bf(x), (int)M, (int)K, bf(w), (int)N, nullptr, false, part.has_value() ? &n : nullptr,
-                            &rp, fp8, cur_stream());
+                            &rp, fp8, cur_stream(), wsc);
 }
 
 // y = x @ w.T on MFMA (gemm.hip); swiglu as gemv.  stages = depth of the LDS-DMA ring (2..4)
@@ -801,16 +823,16 @@ TORCH_LIBRARY(chronos, m) {
           "Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, int hq, int hkv, bool write_q, "
           "float k_scale=1.0, float v_scale=1.0) -> ()");
     m.def("silu_mul(Tensor gate_up) -> Tensor");
-    m.def("gemv(Tensor x, Tensor w, bool swiglu) -> Tensor");
+    m.def("gemv(Tensor x, Tensor w, bool swiglu, Tensor? ws=None) -> Tensor");
     m.def("gemm(Tensor x, Tensor w, bool swiglu, int stages=3) -> Tensor");
     m.def("gemm_pp(Tensor x, Tensor w, int mode, int cfg, int splitk, Tensor? resid, Tensor? part_in, float eps, bool prio) -> (Tensor, Tensor)");
     m.def("gemm_skinny(Tensor x, Tensor w, int mode, int cfg, int splitk, Tensor? resid, Tensor? part_in, float eps) "
           "-> (Tensor, Tensor)");
-    m.def("gemv_resid(Tensor x, Tensor w, Tensor resid_in, Tensor(a!) resid_out) -> Tensor");
-    m.def("gemv_normp(Tensor s, Tensor part, float eps, Tensor w, bool swiglu) -> Tensor");
+    m.def("gemv_resid(Tensor x, Tensor w, Tensor resid_in, Tensor(a!) resid_out, Tensor? ws=None) -> Tensor");
+    m.def("gemv_normp(Tensor s, Tensor part, float eps, Tensor w, bool swiglu, Tensor? ws=None) -> Tensor");
     m.def("qkv_rope(Tensor x, Tensor? part, float eps, Tensor w, Tensor pos, Tensor tok_seq, "
           "Tensor block_table, Tensor cos_sin, Tensor(a!) q_out, Tensor(b!) k_cache, Tensor(c!) v_cache, int hq, "
-          "int hkv, float k_scale=1.0, float v_scale=1.0) -> ()");
+          "int hkv, float k_scale=1.0, float v_scale=1.0, Tensor? ws=None) -> ()");
     m.def("set_decode_gate(Tensor? state, int n) -> ()", &set_decode_gate);
     m.def("attn_init() -> ()", [] { chronos::attn_init(); });
     m.def("quant_rows(Tensor x, Tensor(a!)? resid, Tensor? w, float eps, int mode) -> (Tensor, Tensor)");

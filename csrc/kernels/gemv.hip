@@ -20,6 +20,7 @@
 namespace chronos {
 
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 template <typename T>
 __device__ __forceinline__ T ld_nt(const T* p) {
@@ -38,6 +39,30 @@ __device__ __forceinline__ float dot8(const u16x8& w, const u16x8& x, float acc)
                                           acc, false);
     acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_shufflevector(wb, wb, 6, 7), __builtin_shufflevector(xb, xb, 6, 7),
                                           acc, false);
+    return acc;
+}
+
+// W8A16: 16 e4m3 weights (one 16-B piece) against 16 bf16 activations (two pieces); the weights become bf16 pairs
+// with v_cvt_scalef32_pk_bf16_fp8 (exact: e4m3 fits bf16) and meet x in the same v_dot2_f32_bf16 as dot8
+__device__ __forceinline__ float qdot16(const u16x8& w, const u16x8& x0, const u16x8& x1, float acc) {
+    const i32x4 wi = __builtin_bit_cast(i32x4, w);
+    const bf16x8 a = __builtin_bit_cast(bf16x8, x0), b = __builtin_bit_cast(bf16x8, x1);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(wi[0], 1.f, false),
+                                          __builtin_shufflevector(a, a, 0, 1), acc, false);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(wi[0], 1.f, true),
+                                          __builtin_shufflevector(a, a, 2, 3), acc, false);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(wi[1], 1.f, false),
+                                          __builtin_shufflevector(a, a, 4, 5), acc, false);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(wi[1], 1.f, true),
+                                          __builtin_shufflevector(a, a, 6, 7), acc, false);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(wi[2], 1.f, false),
+                                          __builtin_shufflevector(b, b, 0, 1), acc, false);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(wi[2], 1.f, true),
+                                          __builtin_shufflevector(b, b, 2, 3), acc, false);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(wi[3], 1.f, false),
+                                          __builtin_shufflevector(b, b, 4, 5), acc, false);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(wi[3], 1.f, true),
+                                          __builtin_shufflevector(b, b, 6, 7), acc, false);
     return acc;
 }
 
@@ -60,7 +85,12 @@ enum : int { kPlain = 0, kSwiglu = 1, kRope = 2, kRope8 = 3, kResid = 4 };
 // smaller grid whose workgroups loop over groups g, g + grid, ...  In the loop the NEXT group's first weight ring is
 // issued as soon as the current group's last dot products have consumed the ring, so its loads are in flight during
 // the current group's cross-wave reduction, barrier and epilogue (the weight stream does not stop between groups).
-template <int M, int R, int MODE, bool NORMP>
+//
+// WQ (W8A16, the fp8-weight decode step): W is e4m3 bytes with a per-row scale (nrm.wscale).  A lane's 16-B weight
+// piece is then 16 elements, a chunk 1024 elements, and x comes as two 16-B pieces per chunk; every fused epilogue is
+// the same, the row sums scaled by their row's weight scale first.  Half the weight bytes of the bf16 kernel, no
+// activation quantisation launch (the W8A8 qgemv path needs one per projection).
+template <int M, int R, int MODE, bool NORMP, bool WQ = false>
 __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ x, int mrows, int K,
                                                    const uint16_t* __restrict__ W, uint16_t* __restrict__ y,
                                                    int nout, int half, GemvNorm nrm, GemvRope rp,
@@ -74,7 +104,8 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
     constexpr int NR = SWIGLU ? 2 * R : R;  // weight rows streamed per group
     constexpr int V = NR * M;               // partial sums per lane
     // register ring depth (VGPR budget): M = 2 with 8 rows at depth 3 took all 256 VGPRs (one wave per SIMD)
-    constexpr int DEPTH = (NR + M) * 4 < 40 ? 3 : 2;
+    constexpr int XV = WQ ? 2 : 1;         // 16-B x pieces per lane per chunk
+    constexpr int DEPTH = (NR + XV * M) * 4 < 40 ? 3 : 2;
     // gn < 0: check the decode gate BEFORE the first weight loads (a closed gate then streams no weights; an open one
     // pays the state read's latency up front).  gn > 0: after them (below).
     if (gn < 0 && gate_closed(gst, -gn)) return;
@@ -82,28 +113,33 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
     if (g >= ngroups) return;
     __shared__ float red[4][V];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int nchunk = K >> 9;  // 512-element (1 KiB) chunks per row
+    const int nchunk = WQ ? K >> 10 : K >> 9;  // 1 KiB weight chunks per row (512 bf16 / 1024 e4m3 elements)
+    // weight row of the group's r-th streamed row
+    auto rowidx = [&](int bid, int r) {
+        if constexpr (ROPE) return (bid / RWG) * 128 + (r < RP ? 0 : 64) + RP * (bid % RWG) + (r % RP);
+        else return (SWIGLU && r >= R) ? half + bid * R + (r - R) : bid * R + r;
+    };
     // row bases are wave-uniform (SGPR pairs); the per-lane part is one 32-bit offset (lane + 64 * chunk) * 16 B
     const u16x8* wrow[NR];
     auto set_rows = [&](int bid) {
-        const int n0 = bid * R;
 #pragma unroll
-        for (int r = 0; r < NR; ++r) {
-            int row;
-            if constexpr (ROPE) row = (bid / RWG) * 128 + (r < RP ? 0 : 64) + RP * (bid % RWG) + (r % RP);
-            else row = (SWIGLU && r >= R) ? half + n0 + (r - R) : n0 + r;
-            wrow[r] = reinterpret_cast<const u16x8*>(W + (int64_t)row * K);
-        }
+        for (int r = 0; r < NR; ++r)
+            wrow[r] = reinterpret_cast<const u16x8*>(reinterpret_cast<const uint8_t*>(W) +
+                                                     (int64_t)rowidx(bid, r) * K * (WQ ? 1 : 2));
     };
     const u16x8* xr = reinterpret_cast<const u16x8*>(x);
     const int xstride = K >> 3;
-    u16x8 wr[DEPTH][NR], xv[DEPTH][M];
+    u16x8 wr[DEPTH][NR], xv[DEPTH][M][XV];
     auto load = [&](int c, int d) {
         const int off = c * 64 + lane;
 #pragma unroll
         for (int r = 0; r < NR; ++r) wr[d][r] = ld_nt(wrow[r] + off);
 #pragma unroll
-        for (int m = 0; m < M; ++m) xv[d][m] = m < mrows ? xr[m * xstride + off] : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        for (int m = 0; m < M; ++m)
+#pragma unroll
+            for (int v = 0; v < XV; ++v)
+                xv[d][m][v] = m < mrows ? xr[m * xstride + (WQ ? c * 128 + 2 * lane + v : off)]
+                                        : u16x8{0, 0, 0, 0, 0, 0, 0, 0};
     };
     // wave w takes chunks w, w+4, w+8, ... of every row
     auto prologue = [&]() {
@@ -163,12 +199,23 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
 #pragma unroll
                     for (int r = 0; r < NR; ++r)
 #pragma unroll
-                        for (int m = 0; m < M; ++m) acc[r * M + m] = dot8(wr[d][r], xv[d][m], acc[r * M + m]);
+                        for (int m = 0; m < M; ++m) {
+                            if constexpr (WQ)
+                                acc[r * M + m] = qdot16(wr[d][r], xv[d][m][0], xv[d][m][1], acc[r * M + m]);
+                            else
+                                acc[r * M + m] = dot8(wr[d][r], xv[d][m][0], acc[r * M + m]);
+                        }
                     if (c + 4 * DEPTH < nchunk) load(c + 4 * DEPTH, d);
                 }
             }
         }
         const int bid = g, n0 = g * R;
+        // the row sum of output i (= r * M + m) with its row's fp8 weight scale
+        auto totw = [&](int i) {
+            float v = tot(i);
+            if constexpr (WQ) v *= nrm.wscale[rowidx(bid, i / M)];
+            return v;
+        };
         g += gridDim.x;
         const bool more = g < ngroups;
         if (more) {  // the ring is consumed: start the next group's weight stream before this group's epilogue
@@ -187,7 +234,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
             const int pr = t / M, m = t % M;
             if (t < RP * M && m < mrows) {
                 const int unit = bid / RWG, d = RP * (bid % RWG) + pr;  // head (q | k | v), dim in [0, 64)
-                const float x1 = bf2f(f2bf(tot(pr * M + m))), x2 = bf2f(f2bf(tot((pr + RP) * M + m)));
+                const float x1 = bf2f(f2bf(totw(pr * M + m))), x2 = bf2f(f2bf(totw((pr + RP) * M + m)));
                 const int p = rp.pos[m];
                 const int64_t blk = rp.bt[(int64_t)rp.tok_seq[m] * rp.bt_stride + p / rp.bs];
                 const int off = p % rp.bs;
@@ -233,7 +280,7 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
                 float v = 0.f;
                 if (m < mrows) {
                     const int64_t i = (int64_t)m * nout + n0 + r;
-                    const uint16_t sb = f2bf(bf2f(f2bf(tot(t))) + bf2f(nrm.rin[i]));
+                    const uint16_t sb = f2bf(bf2f(f2bf(totw(t))) + bf2f(nrm.rin[i]));
                     nrm.rout[i] = sb;
                     v = bf2f(sb) * bf2f(sb);
                 }
@@ -250,9 +297,9 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
             for (int t = threadIdx.x; t < R * M; t += 256) {
                 const int r = t / M, m = t % M;
                 if (m >= mrows) continue;
-                const float gv = tot(r * M + m);
+                const float gv = totw(r * M + m);
                 if constexpr (SWIGLU) {
-                    const float u = tot((R + r) * M + m);
+                    const float u = totw((R + r) * M + m);
                     const float gb = bf2f(f2bf(gv)), ub = bf2f(f2bf(u));  // the unfused path rounds the GEMM outputs
                     const float sg = bf2f(f2bf(gb / (1.f + __expf(-gb))));
                     y[(int64_t)m * nout + n0 + r] = f2bf(sg * ub);
@@ -293,13 +340,14 @@ static int rows_knob(const char* name, int dflt) {
     return (v == 1 || v == 2 || v == 4 || v == 8 || v == 16) ? v : dflt;
 }
 
-template <int M>
+template <int M, bool WQ = false>
 static void launch_m(const uint16_t* x, int mrows, int K, const uint16_t* W, int N, uint16_t* y, int mode,
-                     const GemvNorm* nrm, const GemvRope* rp, hipStream_t st) {
+                     const GemvNorm* nrm, const GemvRope* rp, hipStream_t st, const float* wscale = nullptr) {
     constexpr int R1 = rows_plain<M>(), R2 = rows_swiglu<M>();
     const GemvNorm nz{};
     const GemvRope rz{};
-    const GemvNorm na = nrm ? *nrm : nz;
+    GemvNorm na = nrm ? *nrm : nz;
+    na.wscale = wscale;
     const GemvRope ra = rp ? *rp : rz;
     const bool np = nrm && nrm->part;  // consumer of a kResid producer
     const int32_t* gst = g_gate_n > 0 && g_gate_n <= kGateMax ? g_gate_state : nullptr;
@@ -315,9 +363,10 @@ static void launch_m(const uint16_t* x, int mrows, int K, const uint16_t* W, int
     const int persist = knob("gemv_persist", -1);
 #define GV(MODE_, NP_, RR, GRID, NOUT, HALF)                                                                     \
     do {                                                                                                         \
-        const int fit_ = resident_workgroups(gemv_kernel<M, RR, MODE_, NP_>, 256);                              \
+        const int fit_ = resident_workgroups(gemv_kernel<M, RR, MODE_, NP_, WQ>, 256);                          \
         const int cap_ = persist == 0 ? (GRID) : persist > 0 && persist < fit_ ? persist : fit_;                 \
-        hipLaunchKernelGGL((gemv_kernel<M, RR, MODE_, NP_>), dim3(cap_ < (GRID) ? cap_ : (GRID)), dim3(256), 0,  \
+        hipLaunchKernelGGL((gemv_kernel<M, RR, MODE_, NP_, WQ>), dim3(cap_ < (GRID) ? cap_ : (GRID)), dim3(256), \
+                           0,                                                                                    \
                            st, x, mrows, K, W, y, NOUT, HALF, na, ra, gst, gn, (GRID));                          \
     } while (0)
     if (mode == kSwiglu) {
@@ -406,9 +455,14 @@ void launch_gemv(const uint16_t* x, int M, int K, const uint16_t* W, int N, uint
 }
 
 void launch_gemv_ex(const uint16_t* x, int M, int K, const uint16_t* W, int N, uint16_t* y, bool swiglu,
-                    const GemvNorm* nrm, const GemvRope* rope, bool fp8, hipStream_t st) {
+                    const GemvNorm* nrm, const GemvRope* rope, bool fp8, hipStream_t st, const float* wscale) {
     if (M <= 0) return;
     const int mode = rope ? (fp8 ? kRope8 : kRope) : swiglu ? kSwiglu : kPlain;
+    if (wscale) {
+        if (M == 1) launch_m<1, true>(x, M, K, W, N, y, mode, nrm, rope, st, wscale);
+        else launch_m<2, true>(x, M, K, W, N, y, mode, nrm, rope, st, wscale);
+        return;
+    }
     if (M == 1) launch_m<1>(x, M, K, W, N, y, mode, nrm, rope, st);
     else launch_m<2>(x, M, K, W, N, y, mode, nrm, rope, st);
 }
@@ -416,13 +470,16 @@ void launch_gemv_ex(const uint16_t* x, int M, int K, const uint16_t* W, int N, u
 int gemv_resid_parts(int M, int N) { return N / (M == 1 ? resid_rows(N) : M <= 2 ? rows_plain<2>() : rows_plain<4>()); }
 
 int launch_gemv_resid(const uint16_t* x, int M, int K, const uint16_t* W, int N, const uint16_t* rin, uint16_t* rout,
-                      float* part_out, hipStream_t st) {
+                      float* part_out, hipStream_t st, const float* wscale) {
     if (M <= 0) return 0;
     GemvNorm nrm{};
     nrm.rin = rin;
     nrm.rout = rout;
     nrm.part_out = part_out;
-    if (M == 1) launch_m<1>(x, M, K, W, N, nullptr, kResid, &nrm, nullptr, st);
+    if (wscale) {
+        if (M == 1) launch_m<1, true>(x, M, K, W, N, nullptr, kResid, &nrm, nullptr, st, wscale);
+        else launch_m<2, true>(x, M, K, W, N, nullptr, kResid, &nrm, nullptr, st, wscale);
+    } else if (M == 1) launch_m<1>(x, M, K, W, N, nullptr, kResid, &nrm, nullptr, st);
     else launch_m<2>(x, M, K, W, N, nullptr, kResid, &nrm, nullptr, st);
     return gemv_resid_parts(M, N);
 }

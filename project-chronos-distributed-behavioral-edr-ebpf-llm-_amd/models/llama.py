@@ -28,7 +28,10 @@ from ..parallel.tp import TPContext
 # decode steps (T <= 2, TP=1): residual add + norm partials in the producing GEMV's epilogue, the norm in the consuming
 # GEMV's prologue, RoPE + paged-KV write in the QKV GEMV's epilogue (CHRONOS_FUSE_NORM=0: the separate kernels)
 _FUSE_NORM = os.environ.get("CHRONOS_FUSE_NORM", "1") != "0"
-_FUSE_AR_NORM = os.environ.get("CHRONOS_FUSE_AR_NORM", "1") != "0"  # TP: fused IPC all-reduce + residual + RMSNorm
+_FUSE_AR_NORM = os.environ.get("CHRONOS_FUSE_AR_NORM", "1") != "0"
+# fp8-weight decode (T <= 2): W8A16 GEMVs on bf16 activations with the bf16 path's fused epilogues (norm / RoPE + KV
+# write / residual) instead of W8A8 (an activation-quantisation launch per projection)
+_W8A16_DECODE = os.environ.get("CHRONOS_W8A16_DECODE", "1") != "0"  # TP: fused IPC all-reduce + residual + RMSNorm
 # batched decode (>= 2048 (row, kv head) items, bf16 KV): RoPE + paged-KV write fused into the decode attention
 _FUSE_DECODE_ROPE = os.environ.get("CHRONOS_FUSE_DECODE_ROPE", "1") != "0"
 
@@ -581,7 +584,7 @@ class LlamaModel:
             st["resid"] = h.s
             return ops.LazyNorm(h.s, h.part, w, eps)
         resid = None if first else st["resid"]
-        if self.w.fp8:
+        if self.w.fp8 and not st.get("w16"):
             return ops.quant_rows(h, resid, w, eps, 1 if resid is None else 2)
         return ops.rmsnorm(h, w, eps) if resid is None else ops.add_rmsnorm(h, resid, w, eps)
 
@@ -592,7 +595,7 @@ class LlamaModel:
         applies it as a per-row scale."""
         T = st["T"]
         if (_FUSE_NORM and self.w.norms_folded and self.tp.world == 1 and x.is_cuda and st["sb"].cp is None
-                and (st["sb"].tiles is None or T > 2) and ops.resid_ok(T, w.shape[0], w.shape[1])):
+                and (st["sb"].tiles is None or T > 2) and ops.resid_ok(T, w.shape[0], w.shape[1], ops.is_q(w))):
             return ops.gemv_resid(x, w, st["resid"])
         return ops.linear(x, w)
 
@@ -627,7 +630,8 @@ class LlamaModel:
         runs the projections over prefill and decode rows together and the attention of each part with its own
         kernel (flash / split-K prefill tiles; the decode kernel for the one-token rows)."""
         sb, T, x = st["sb"], st["T"], st["x"]
-        if (sb.dec is None and not self.w.fp8 and _FUSE_NORM and ops.qkv_rope(
+        q8 = self.w.fp8 and not st.get("w16")  # W8A8: x is (e4m3 bytes, row scales)
+        if (sb.dec is None and not q8 and _FUSE_NORM and ops.qkv_rope(
                 x, lw.wqkv, sb.pos, sb.tok_seq, sb.block_table, self.cos_sin, st["q_buf"], kv.k[li], kv.v[li],
                 self.hq, self.hkv, kv.k_scale[li], kv.v_scale[li])):
             # decode: QKV GEMV (+ folded norm) + RoPE / paged-KV write in one launch
@@ -637,21 +641,21 @@ class LlamaModel:
         else:
             # a LazyNorm input goes straight to the projection (the batched GEMM applies the folded norm as a row
             # scale; anything else materialises it)
-            qkv = ops.qlinear(*x, lw.wqkv.q, lw.wqkv.s) if self.w.fp8 else ops.linear(x, lw.wqkv)
+            qkv = ops.qlinear(*x, lw.wqkv.q, lw.wqkv.s) if q8 else ops.linear(x, lw.wqkv)
             if sb.dec is None:
                 attn = self._attn_rows(li, qkv, sb, st["q_buf"], kv)
             else:
                 tp_ = T - sb.dec.ntiles
                 attn = torch.cat([self._attn_rows(li, qkv[:tp_], sb, st["q_buf"][:tp_], kv),
                                   self._attn_rows(li, qkv[tp_:], sb.dec, st["q_buf"][tp_:], kv)])
-        if self.w.fp8:
+        if q8:
             return ops.qlinear(*ops.quant_rows(attn), lw.wo.q, lw.wo.s)
         return self._out_proj(attn, lw.wo, st)
 
     def _mlp(self, lw: LayerWeights, st: dict) -> torch.Tensor:
         """SwiGLU MLP up to the row-parallel down_proj; returns this rank's partial sum."""
         x = st["x"]
-        if self.w.fp8:
+        if self.w.fp8 and not st.get("w16"):
             return ops.qlinear(*ops.qgate_up_quant(*x, lw.w_gu.q, lw.w_gu.s), lw.w_down.q, lw.w_down.s)
         return self._out_proj(ops.gate_up_silu(x, lw.w_gu), lw.w_down, st)
 
@@ -782,7 +786,9 @@ class LlamaModel:
             ids = p.ids if p.dec is None else torch.cat([p.ids, p.dec.ids])
             h = tp.all_reduce(ops.embedding(ids, w.embed, w.vocab_start))
             T = ids.numel()
-            st = dict(sb=p, T=T, resid=h, q_buf=torch.empty(T, self.hq, cfg.head_dim, device=h.device, dtype=h.dtype))
+            st = dict(sb=p, T=T, resid=h, q_buf=torch.empty(T, self.hq, cfg.head_dim, device=h.device, dtype=h.dtype),
+                      w16=(w.fp8 and _W8A16_DECODE and T <= 2 and h.is_cuda and p.cp is None and p.dec is None
+                           and cfg.hidden_size % 1024 == 0))
             st["x"] = self._norm(h, st, w.layers[0].attn_norm, first=True)
             states.append(st)
         L = len(w.layers)

@@ -14,7 +14,8 @@ import os
 import torch
 
 from . import reference as ref
-from .gemm import LazyNorm, ResidOut, gate_up_silu, gemv_ok, gemv_resid, linear, resid_ok  # noqa: F401  (re-export)
+from .gemm import (LazyNorm, ResidOut, gate_up_silu, gemv_ok, gemv_q_ok, gemv_resid, is_q, linear,  # noqa: F401
+                   resid_ok)
 
 _loaded = False
 
@@ -186,10 +187,12 @@ def qkv_rope(x, w_qkv, pos, tok_seq, block_table, cos_sin, q_out, k_cache, v_cac
         return False
     t = x.s if lazy else x
     m, n, k = t.numel() // t.shape[-1], w_qkv.shape[0], t.shape[-1]
-    if not (t.is_cuda and m <= 2 and gemv_ok(m, n, k)):
+    fp8w = is_q(w_qkv)  # fp8 weights: the W8A16 GEMV (e4m3 bytes + per-row scales)
+    if not (t.is_cuda and m <= 2 and (gemv_q_ok(m, n, k) if fp8w else gemv_ok(m, n, k))):
         return False
-    _k().qkv_rope(t.reshape(m, k), x.part if lazy else None, x.eps if lazy else 0.0, w_qkv,
-                  pos, tok_seq, block_table, cos_sin, q_out, k_cache, v_cache, hq, hkv, k_scale, v_scale)
+    _k().qkv_rope(t.reshape(m, k), x.part if lazy else None, x.eps if lazy else 0.0, w_qkv.q if fp8w else w_qkv,
+                  pos, tok_seq, block_table, cos_sin, q_out, k_cache, v_cache, hq, hkv, k_scale, v_scale,
+                  w_qkv.s if fp8w else None)
     return True
 
 

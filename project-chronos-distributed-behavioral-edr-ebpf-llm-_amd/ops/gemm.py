@@ -245,12 +245,37 @@ class LazyNorm:
         return x.materialize() if isinstance(x, LazyNorm) else x
 
 
+def is_q(w) -> bool:
+    """An fp8 projection weight (models/llama.py QTensor: e4m3 bytes ``q`` [N, K] + per-row scales ``s``)."""
+    return not isinstance(w, torch.Tensor) and hasattr(w, "q") and hasattr(w, "s")
+
+
+def gemv_q_ok(m: int, n: int, k: int) -> bool:
+    """Shapes of the W8A16 decode GEMV (gemv.hip WQ: fp8 weights, bf16 activations): one or two rows, whole 1 KiB
+    weight chunks."""
+    return m <= 2 and k % 1024 == 0 and n % 16 == 0
+
+
+def _q_fallback(x, w, swiglu: bool = False) -> torch.Tensor:
+    """fp8 weight off the W8A16 GEMV shapes: quantise the activations and run the W8A8 op."""
+    from . import qlinear, quant_rows
+
+    xq, xs = quant_rows(LazyNorm.force(x).reshape(-1, w.shape[1]))
+    y = qlinear(xq, xs, w.q, w.s, swiglu)
+    return y.view(*x.shape[:-1], y.shape[-1])
+
+
 def gemv_resid(x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor) -> ResidOut:
     """Producer (O / down projection, TP=1): the new residual stream s = bf16(bf16(x @ w.T) + resid) and the RMSNorm
-    partial sums of s^2, in one launch — the GEMV at M <= 2, the batched GEMM's kResid epilogue above."""
+    partial sums of s^2, in one launch — the GEMV at M <= 2, the batched GEMM's kResid epilogue above.  ``w`` may be
+    an fp8 QTensor at the W8A16 GEMV shapes (resid_ok(..., fp8=True))."""
     from . import _k
 
     m, k = x.numel() // x.shape[-1], x.shape[-1]
+    if is_q(w):
+        s = torch.empty(resid.shape, dtype=resid.dtype, device=resid.device)
+        part = _k().gemv_resid(x.reshape(-1, k), w.q, resid, s, w.s)
+        return ResidOut(s, part)
     if m > GEMV_MAX_M:
         s, part = pp_gemm(x, w, PP_RESID, pp_plan(m, w.shape[0], k, PP_RESID), resid.reshape(m, -1))
         return ResidOut(s.view(resid.shape), part)
@@ -259,9 +284,11 @@ def gemv_resid(x: torch.Tensor, w: torch.Tensor, resid: torch.Tensor) -> ResidOu
     return ResidOut(s, part)
 
 
-def resid_ok(m: int, n: int, k: int) -> bool:
+def resid_ok(m: int, n: int, k: int, fp8: bool = False) -> bool:
     """Shapes of the residual-epilogue producer: the M <= 2 GEMV shapes (gemv.hip kResid) and the batched GEMM's
-    (gemm_pp.hip kResid) where the plan takes it."""
+    (gemm_pp.hip kResid) where the plan takes it; fp8 weights: the W8A16 GEMV shapes only."""
+    if fp8:
+        return m <= GEMV_MAX_M and gemv_q_ok(m, n, k)
     if m <= GEMV_MAX_M:
         return gemv_ok(m, n, k)
     return pp_plan(m, n, k, PP_RESID) is not None
@@ -301,6 +328,15 @@ def gate_up_silu(x: torch.Tensor, w_gu: torch.Tensor) -> torch.Tensor:
     SwiGLU epilogue above, with the folded input norm when x is a LazyNorm), else GEMM + silu_mul."""
     from . import _k, silu_mul
 
+    if is_q(w_gu):  # fp8 weights: the W8A16 GEMV (folded norm fused when x is a LazyNorm), else W8A8
+        m, n, k = (x.rows() if isinstance(x, LazyNorm) else x.numel() // x.shape[-1]), w_gu.shape[0], x.shape[-1]
+        if isinstance(x, LazyNorm) and x.fusable() and gemv_q_ok(m, n, k):
+            return _k().gemv_normp(x.s, x.part, x.eps, w_gu.q, True, w_gu.s)
+        x = LazyNorm.force(x)
+        if x.is_cuda and gemv_q_ok(m, n, k):
+            y = _k().gemv(x.reshape(-1, k), w_gu.q, True, w_gu.s)
+            return y.view(*x.shape[:-1], y.shape[-1])
+        return _q_fallback(x, w_gu, True)
     if isinstance(x, LazyNorm):
         m, n, k = x.rows(), w_gu.shape[0], x.shape[-1]
         if x.fusable() and gemv_ok(m, n, k, swiglu=True):
@@ -324,6 +360,17 @@ def gate_up_silu(x: torch.Tensor, w_gu: torch.Tensor) -> torch.Tensor:
 
 
 def linear(x, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    if is_q(w):  # fp8 weights: the W8A16 GEMV (folded norm fused when x is a LazyNorm), else W8A8
+        from . import _k
+
+        m, n, k = (x.rows() if isinstance(x, LazyNorm) else x.numel() // x.shape[-1]), w.shape[0], x.shape[-1]
+        if isinstance(x, LazyNorm) and x.fusable() and gemv_q_ok(m, n, k):
+            return _k().gemv_normp(x.s, x.part, x.eps, w.q, False, w.s)
+        x = LazyNorm.force(x)
+        if x.is_cuda and gemv_q_ok(m, n, k):
+            y = _k().gemv(x.reshape(-1, k), w.q, False, w.s)
+            return y.view(*x.shape[:-1], n)
+        return _q_fallback(x, w)
     if isinstance(x, LazyNorm):
         m, n, k = x.rows(), w.shape[0], x.shape[-1]
         if x.fusable() and out is None and gemv_ok(m, n, k):

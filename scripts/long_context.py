@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--cp", type=int, default=1, help="context-parallel ranks (torch.distributed.run)")
     ap.add_argument("--repeat", type=int, default=1, help="run the long request this many times (first = cold)")
     ap.add_argument("--no-jump-forward", action="store_true")
+    ap.add_argument("--knob", action="append", default=[], help="kernel knob name=value (torch.ops.chronos.set_knob)")
     a = ap.parse_args()
     from chronos.brain.engine.engine import Engine, EngineConfig
     from chronos.parallel.tp import TPContext
@@ -60,6 +61,9 @@ def main():
                               cp_min_tokens=min(4096, a.chunk), weight_dtype=a.weights,
                               jump_forward=not a.no_jump_forward),
                  cp=cp)
+    for kv in a.knob:
+        name, val = kv.split("=")
+        torch.ops.chronos.set_knob(name, int(val))
     # a very long chain: concatenated fleet histories (one process tree that never triggered a reset)
     hist = []
     for c in synthetic_chains(6000, seed=42):
