@@ -42,6 +42,9 @@ void launch_gemv_ex(const uint16_t* x, int M, int K, const uint16_t* W, int N, u
 // producer: rout = bf16(bf16(x @ W^T) + rin), part_out[m, wg] = per-workgroup sum of rout^2; returns nparts
 int launch_gemv_resid(const uint16_t* x, int M, int K, const uint16_t* W, int N, const uint16_t* rin, uint16_t* rout,
                       float* part_out, hipStream_t st, const float* wscale = nullptr);
-int gemv_resid_parts(int M, int N);
+int gemv_resid_parts(int M, int N, bool wq = false);
+// W8A16 plain / SwiGLU GEMV for M <= 4 rows (jump-forward forwards of the fp8-weight model): W e4m3 bytes [N, K]
+void launch_gemv_q(const uint16_t* x, int M, int K, const uint8_t* W, const float* wscale, int N, uint16_t* y,
+                   bool swiglu, hipStream_t st);
 
 }  // namespace chronos

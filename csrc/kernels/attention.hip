@@ -33,12 +33,12 @@ __device__ __forceinline__ void combine_tile(const float* __restrict__ part_o, c
                                              int qlen, int hq, int hkv, int nsplit, int ntiles) {
     constexpr int ROWS = NQT * 16;
     const int G = hq / hkv;
-    if (NQT == 1 && qlen == 1 && rel0 == 0 && G <= 16) {
-        // decode (one query row per sequence): only G of the 16 rows are live, so the G x 16 (row, 8-column group)
-        // items take P adjacent lanes each, the lanes split the splits between them and merge through shuffles —
-        // P times fewer dependent global-load rounds than one lane walking all nsplit partials (128k decode: 32
-        // splits x 8 kv heads, 17.5 -> a few us per layer)
-        const int items = G * 16;
+    if (NQT == 1 && rel0 == 0 && qlen * G <= 16) {
+        // decode (one query row per sequence, or qlen <= 16 / G tokens of one sequence): only qlen x G of the 16
+        // rows are live, so the (row, 8-column group) items take P adjacent lanes each, the lanes split the splits
+        // between them and merge through shuffles — P times fewer dependent global-load rounds than one lane walking
+        // all nsplit partials (128k decode: 32 splits x 8 kv heads, 17.5 -> a few us per layer)
+        const int items = qlen * G * 16;
         const int P = items <= 16 ? 16 : items <= 32 ? 8 : items <= 64 ? 4 : items <= 128 ? 2 : 1;
         const int item = threadIdx.x / P, sub = threadIdx.x % P;
         const bool live = item < items;
@@ -77,7 +77,7 @@ __device__ __forceinline__ void combine_tile(const float* __restrict__ part_o, c
             u16x8 ov;
 #pragma unroll
             for (int j = 0; j < 8; ++j) ov[j] = f2bf(acc[j] * inv);
-            *reinterpret_cast<u16x8*>(out + ((int64_t)qbase * hq + h * G + row) * kD + c8 * 8) = ov;
+            *reinterpret_cast<u16x8*>(out + ((int64_t)(qbase + row / G) * hq + h * G + row % G) * kD + c8 * 8) = ov;
         }
         return;
     }
@@ -406,7 +406,11 @@ __global__ void __launch_bounds__(256, 1) split_decode_kernel(
     const uint16_t* __restrict__ q, const void* __restrict__ kcv, const void* __restrict__ vcv,
     const int32_t* __restrict__ block_table, int bt_stride, const int32_t* __restrict__ ctx_len,
     uint16_t* __restrict__ out, float* __restrict__ part_o, float* __restrict__ part_lse, int hq, int hkv,
-    float scale_log2, float k_scale, float v_scale, const int32_t* __restrict__ gst, int gn, int* __restrict__ cnt) {
+    float scale_log2, float k_scale, float v_scale, const int32_t* __restrict__ gst, int gn, int* __restrict__ cnt,
+    const int32_t* __restrict__ q_start = nullptr, int mq = 1) {
+    // mq > 1: sequence seq has q_start[seq + 1] - q_start[seq] <= 16 / G query tokens (a jump-forward chunk over a
+    // long context), its last one at the context's end: MFMA column r = token r / G, q head r % G, and column r's
+    // keys stop at ctx - (tokens after it) — one pass over the K/V for all of them instead of one per token
     constexpr int block_size = 16, ROWS = 16;
     constexpr int SB = sd_step_bytes<FP8>();            // bytes of one step in the ring
     constexpr int KB = SB / 2;                          // K part (2 pages); V^T part after it
@@ -419,12 +423,15 @@ __global__ void __launch_bounds__(256, 1) split_decode_kernel(
     const int r = lane & 15, h4 = lane >> 4;
     const int G = hq / hkv, h = blockIdx.y, seq = blockIdx.x, nsplit = gridDim.z;
     const int ctx = ctx_len[seq];
+    const int qb = mq > 1 ? q_start[seq] : seq, ql = mq > 1 ? q_start[seq + 1] - qb : 1;
+    const int tq = r / G, gq = r - tq * G;  // column r: token tq of the sequence, q head gq of the group
+    const int kcap = tq < ql ? ctx - (ql - 1 - tq) : ctx;
     unsigned char* ring = sd_smem_raw + w * NB * SB;  // this wave's ring of NB steps
 
     bf16x8 qf[4];
     {
-        const bool valid = r < G;
-        const uint16_t* qp = q + ((int64_t)seq * hq + h * G + (valid ? r : 0)) * kD + 8 * h4;
+        const bool valid = tq < ql;
+        const uint16_t* qp = q + ((int64_t)(qb + (valid ? tq : 0)) * hq + h * G + (valid ? gq : 0)) * kD + 8 * h4;
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             bf16x8 v = *reinterpret_cast<const bf16x8*>(qp + 32 * c);
@@ -437,6 +444,7 @@ __global__ void __launch_bounds__(256, 1) split_decode_kernel(
     chunk = (chunk + 31) & ~31;
     const int ks = blockIdx.z * chunk;
     const int ke = min(ctx, ks + chunk);
+    const int kl = min(ke, kcap);  // this lane's column: keys past it are masked
     const int32_t* bt = block_table + (int64_t)seq * bt_stride;
     const float sl2 = FP8 ? scale_log2 * k_scale : scale_log2;  // fp8: K's cache scale folded into the score scale
 
@@ -546,7 +554,7 @@ __global__ void __launch_bounds__(256, 1) split_decode_kernel(
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 float v = sc[g][i] * sl2;
-                if (t0 + 16 * g + 4 * h4 + i >= ke) v = -INFINITY;
+                if (t0 + 16 * g + 4 * h4 + i >= kl) v = -INFINITY;
                 sc[g][i] = v;
                 mx = fmaxf(mx, v);
             }
@@ -613,8 +621,8 @@ __global__ void __launch_bounds__(256, 1) split_decode_kernel(
     __syncthreads();
     for (int idx = threadIdx.x; idx < ROWS * 16; idx += 256) {
         const int row = idx >> 4, c8 = idx & 15;
-        if (row >= G) continue;
-        const int hd = h * G + row;
+        if (row >= ql * G) continue;
+        const int64_t orow_out = (int64_t)(qb + row / G) * hq + h * G + row % G;
         float M = -1e30f;
 #pragma unroll
         for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, sm[ww * ROWS + row]);
@@ -632,7 +640,7 @@ __global__ void __launch_bounds__(256, 1) split_decode_kernel(
             u16x8 ov;
 #pragma unroll
             for (int jj = 0; jj < 8; ++jj) ov[jj] = f2bf(acc[jj] * inv);
-            *reinterpret_cast<u16x8*>(out + ((int64_t)seq * hq + hd) * kD + c8 * 8) = ov;
+            *reinterpret_cast<u16x8*>(out + orow_out * kD + c8 * 8) = ov;
         } else {
             const int64_t prow = (((int64_t)blockIdx.z * gridDim.x + seq) * hkv + h) * ROWS + row;
             float* po = part_o + prow * kD + c8 * 8;
@@ -660,14 +668,14 @@ __global__ void __launch_bounds__(256, 1) split_decode_kernel(
     }
     __syncthreads();
     if (!flag[0]) return;
-    combine_tile<1>(part_o, part_lse, out, seq, h, 0, seq, 1, hq, hkv, nsplit, gridDim.x);
+    combine_tile<1>(part_o, part_lse, out, seq, h, 0, qb, ql, hq, hkv, nsplit, gridDim.x);
 }
 
 template <int NQT>
 __global__ void __launch_bounds__(256) paged_attn_combine_kernel(
     const float* __restrict__ part_o, const float* __restrict__ part_lse, const int32_t* __restrict__ q_start,
     const int32_t* __restrict__ tiles, uint16_t* __restrict__ out, int hq, int hkv, int nsplit, int ntiles,
-    const int32_t* __restrict__ gst, int gn) {
+    const int32_t* __restrict__ gst, int gn, int mq = 1) {
     if (gate_closed(gst, gn)) return;
     const int tile = blockIdx.x, h = blockIdx.y;
     int rel0, qbase, qlen;
@@ -676,6 +684,10 @@ __global__ void __launch_bounds__(256) paged_attn_combine_kernel(
         rel0 = tiles[2 * tile + 1];
         qbase = q_start[seq];
         qlen = q_start[seq + 1] - qbase;
+    } else if (mq > 1) {  // split_decode_kernel's multi-token sequences
+        rel0 = 0;
+        qbase = q_start[tile];
+        qlen = q_start[tile + 1] - qbase;
     } else {
         rel0 = 0;
         qbase = tile;
@@ -1266,14 +1278,15 @@ size_t paged_attn_smem(int nqt) { return (size_t)(8 * nqt * 16 + 4 * nqt * 16 * 
 void launch_paged_attn(const uint16_t* q, const void* kc, const void* vc, const int32_t* block_table, int bt_stride,
                        const int32_t* q_start, const int32_t* ctx_len, const int32_t* tiles, int ntiles, int nqt,
                        int nsplit, uint16_t* out, float* part_o, float* part_lse, int hq, int hkv, int block_size,
-                       float scale, bool fp8, float k_scale, float v_scale, hipStream_t st) {
+                       float scale, bool fp8, float k_scale, float v_scale, hipStream_t st, int max_q) {
     if (ntiles == 0) return;
     const float scale_log2 = scale * 1.4426950408889634f;
     // decode without a kv split and enough (seq, kv head) items to fill the chip one wave each (>= 2048 waves:
     // 8 per CU); fewer items keep the split-over-waves form (profiles/r1_attn_decode.json: B=64 x 1k ctx is 1.5x
     // faster there, B >= 256 at 128-512 ctx 1.0-1.3x slower)
     const int nitems = ntiles * hkv;
-    if (tiles == nullptr && nqt == 1 && nsplit == 1 && hq / hkv <= 16 && block_size == 16 && nitems >= 2048) {
+    if (tiles == nullptr && nqt == 1 && nsplit == 1 && max_q == 1 && hq / hkv <= 16 && block_size == 16 &&
+        nitems >= 2048) {
         if (knob("decode_attn_legacy", 0)) goto legacy;  // A/B against the split-over-waves kernel
         const int pf = knob("decode_pf", 0);
         const bool lean = knob("decode_lean", 1) != 0;
@@ -1304,7 +1317,8 @@ void launch_paged_attn(const uint16_t* q, const void* kc, const void* vc, const 
     }
 legacy:
     const dim3 grid(ntiles, hkv, nsplit), block(256);
-    if (tiles == nullptr && nqt == 1 && nsplit > 1 && hq / hkv <= 16 && block_size == 16 && knob("split_lds", 1)) {
+    if (tiles == nullptr && nqt == 1 && hq / hkv <= 16 && block_size == 16 &&
+        (max_q > 1 || (nsplit > 1 && knob("split_lds", 1)))) {
         // long-context decode: the LDS-staged split kernel (lane-linear LDS-DMA, NB steps in flight per wave)
         int* cnt = nsplit <= knob("sd_inkernel_max_split", 4) ? tickets_for((int64_t)ntiles * hkv) : nullptr;
         int nb = knob("split_lds_nb", 0);  // ring depth (steps in flight per wave); <= 0: the default
@@ -1317,7 +1331,7 @@ legacy:
                                                shm) == hipSuccess;                                              \
         (void)attr;                                                                                             \
         hipLaunchKernelGGL(kern, grid, block, shm, st, q, kc, vc, block_table, bt_stride, ctx_len, out, part_o,   \
-                           part_lse, hq, hkv, scale_log2, k_scale, v_scale, CHRONOS_GATE, cnt);                 \
+                           part_lse, hq, hkv, scale_log2, k_scale, v_scale, CHRONOS_GATE, cnt, q_start, max_q); \
     }
         if (fp8) {
             if (nb >= 4) SD_LAUNCH(true, 4) else if (nb == 3) SD_LAUNCH(true, 3) else SD_LAUNCH(true, 2)
@@ -1325,9 +1339,9 @@ legacy:
             if (nb >= 2) SD_LAUNCH(false, 2) else SD_LAUNCH(false, 1)
         }
 #undef SD_LAUNCH
-        if (cnt == nullptr)
+        if (nsplit > 1 && cnt == nullptr)
             hipLaunchKernelGGL(paged_attn_combine_kernel<1>, dim3(ntiles, hkv), block, 0, st, part_o, part_lse,
-                               q_start, tiles, out, hq, hkv, nsplit, ntiles, CHRONOS_GATE);
+                               q_start, tiles, out, hq, hkv, nsplit, ntiles, CHRONOS_GATE, max_q);
         return;
     }
     // in-launch combine (last split merges) only for a few splits: with many splits the per-workgroup agent-scope

@@ -34,7 +34,7 @@ bool launch_decode_attn_rope(const uint16_t*, const int32_t*, const float*, void
                              uint16_t*, float*);
 void launch_paged_attn(const uint16_t*, const void*, const void*, const int32_t*, int, const int32_t*,
                        const int32_t*, const int32_t*, int, int, int, uint16_t*, float*, float*, int, int, int, float,
-                       bool, float, float, hipStream_t);
+                       bool, float, float, hipStream_t, int);
 void launch_constrained_sample(const void*, bool, int64_t, const int32_t*, int, int, const int16_t*, const int16_t*,
                                const int16_t*, int, int32_t*, int32_t*, const float*, const int32_t*, const int32_t*, const float*,
                                int32_t*, int32_t*, int32_t*, int32_t*, int32_t*, int, hipStream_t);
@@ -132,7 +132,7 @@ inline const float* chk_gemv_w(const Tensor& w, const c10::optional<Tensor>& ws,
     chk_gpu(*ws, "ws");
     CHK(w.scalar_type() == at::kByte, "w must be uint8 (e4m3 bytes) when ws is given");
     CHK(ws->scalar_type() == at::kFloat && ws->numel() == w.size(0), "ws must be [N] f32");
-    CHK(K % 1024 == 0 && M <= 2, "fp8-weight GEMV: K % 1024 == 0, M <= 2");
+    CHK(K % 1024 == 0 && M <= 4, "fp8-weight GEMV: K % 1024 == 0, M <= 4 (the fused epilogues: M <= 2)");
     return ws->data_ptr<float>();
 }
 
@@ -272,7 +272,8 @@ Tensor silu_mul(const Tensor& gu) {
 
 Tensor paged_attention(const Tensor& q, const Tensor& k_cache, const Tensor& v_cache, const Tensor& block_table,
                        const Tensor& q_start, const Tensor& ctx_len, const c10::optional<Tensor>& tiles,
-                       int64_t ntiles, int64_t nqt, int64_t nsplit, double scale, double k_scale, double v_scale) {
+                       int64_t ntiles, int64_t nqt, int64_t nsplit, double scale, double k_scale, double v_scale,
+                       int64_t max_q) {
     chk_bf16(q, "q");
     const bool fp8 = chk_kv(k_cache, v_cache);
     chk_i32(block_table, "block_table");
@@ -290,6 +291,9 @@ Tensor paged_attention(const Tensor& q, const Tensor& k_cache, const Tensor& v_c
         chk_i32(*tiles, "tiles");
         CHK(tiles->numel() >= 2 * ntiles, "tiles must be [ntiles, 2]");
         tp = i32(*tiles);
+    } else if (max_q > 1) {
+        CHK(nqt == 1 && max_q * (hq / hkv) <= 16 && bs == 16, "multi-token decode: nqt 1, max_q x GQA group <= 16");
+        CHK(q_start.numel() >= ntiles + 1 && ctx_len.numel() >= ntiles, "multi-token decode: q_start [B + 1], ctx [B]");
     } else {
         CHK(ctx_len.numel() >= ntiles && q.size(0) >= ntiles, "decode mode: one query token per tile");
     }
@@ -313,7 +317,7 @@ Tensor paged_attention(const Tensor& q, const Tensor& k_cache, const Tensor& v_c
                                (int)block_table.size(1), i32(q_start), i32(ctx_len), tp, (int)ntiles, (int)nqt,
                                (int)nsplit, bfm(out), nsplit > 1 ? po.data_ptr<float>() : nullptr,
                                nsplit > 1 ? pl.data_ptr<float>() : nullptr, (int)hq, (int)hkv, (int)bs, (float)scale,
-                               fp8, (float)k_scale, (float)v_scale, cur_stream());
+                               fp8, (float)k_scale, (float)v_scale, cur_stream(), (int)max_q);
     return out;
 }
 
@@ -394,8 +398,8 @@ Tensor gemv(const Tensor& x, const Tensor& w, bool swiglu, const c10::optional<T
     c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
     auto y = at::empty({M, swiglu ? N / 2 : N}, x.options());
     if (wsc)
-        chronos::launch_gemv_ex(bf(x), (int)M, (int)K, bf(w), (int)N, bfm(y), swiglu, nullptr, nullptr, false,
-                                cur_stream(), wsc);
+        chronos::launch_gemv_q(bf(x), (int)M, (int)K, reinterpret_cast<const uint8_t*>(w.data_ptr()), wsc, (int)N,
+                               bfm(y), swiglu, cur_stream());
     else
         chronos::launch_gemv(bf(x), (int)M, (int)K, bf(w), (int)N, bfm(y), swiglu, cur_stream());
     return y;
@@ -429,7 +433,8 @@ Tensor gemv_resid(const Tensor& x, const Tensor& w, const Tensor& resid_in, cons
     CHK(resid_in.numel() == M * N && resid_out.numel() == M * N, "gemv_resid: residuals must be [M, N]");
     CHK(resid_in.data_ptr() != resid_out.data_ptr(), "gemv_resid: out of place only");
     c10::hip::HIPGuardMasqueradingAsCUDA g(x.device());
-    auto part = at::empty({M, chronos::gemv_resid_parts((int)M, (int)N)}, x.options().dtype(at::kFloat));
+    CHK(wsc == nullptr || M <= 2, "gemv_resid: M <= 2");
+    auto part = at::empty({M, chronos::gemv_resid_parts((int)M, (int)N, wsc != nullptr)}, x.options().dtype(at::kFloat));
     chronos::launch_gemv_resid(bf(x), (int)M, (int)K, bf(w), (int)N, bf(resid_in), bfm(resid_out),
                                part.data_ptr<float>(), cur_stream(), wsc);
     return part;
@@ -852,7 +857,7 @@ TORCH_LIBRARY(chronos, m) {
           "Tensor(d!)? casc_l=None) -> Tensor");
     m.def("paged_attention(Tensor q, Tensor k_cache, Tensor v_cache, Tensor block_table, Tensor q_start, "
           "Tensor ctx_len, Tensor? tiles, int ntiles, int nqt, int nsplit, float scale, float k_scale=1.0, "
-          "float v_scale=1.0) -> Tensor");
+          "float v_scale=1.0, int max_q=1) -> Tensor");
     m.def("constrained_sample(Tensor logits, Tensor? row_of_slot, Tensor next, Tensor dist, int done_state, "
           "Tensor(a!) state, Tensor(b!) remaining, Tensor? temperature, Tensor? seed, Tensor(c!) ids, Tensor(d!) pos, "
           "Tensor(e!) ctx, Tensor(f!) nout, Tensor(g!) out_tokens, Tensor? topk=None, Tensor? topp=None, "

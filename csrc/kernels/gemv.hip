@@ -42,27 +42,28 @@ __device__ __forceinline__ float dot8(const u16x8& w, const u16x8& x, float acc)
     return acc;
 }
 
-// W8A16: 16 e4m3 weights (one 16-B piece) against 16 bf16 activations (two pieces); the weights become bf16 pairs
-// with v_cvt_scalef32_pk_bf16_fp8 (exact: e4m3 fits bf16) and meet x in the same v_dot2_f32_bf16 as dot8
-__device__ __forceinline__ float qdot16(const u16x8& w, const u16x8& x0, const u16x8& x1, float acc) {
+// W8A16: a 16-B piece of 16 e4m3 weights becomes 8 bf16 pairs with v_cvt_scalef32_pk_bf16_fp8 (exact: e4m3 fits
+// bf16) — once per piece, shared by the M activation rows — and meets x (two 16-B pieces) in the same
+// v_dot2_f32_bf16 as dot8
+__device__ __forceinline__ void q2bf(const u16x8& w, bf16x2_t (&wb)[8]) {
     const i32x4 wi = __builtin_bit_cast(i32x4, w);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        wb[2 * j] = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(wi[j], 1.f, false);
+        wb[2 * j + 1] = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(wi[j], 1.f, true);
+    }
+}
+
+__device__ __forceinline__ float dot16(const bf16x2_t (&wb)[8], const u16x8& x0, const u16x8& x1, float acc) {
     const bf16x8 a = __builtin_bit_cast(bf16x8, x0), b = __builtin_bit_cast(bf16x8, x1);
-    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(wi[0], 1.f, false),
-                                          __builtin_shufflevector(a, a, 0, 1), acc, false);
-    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(wi[0], 1.f, true),
-                                          __builtin_shufflevector(a, a, 2, 3), acc, false);
-    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(wi[1], 1.f, false),
-                                          __builtin_shufflevector(a, a, 4, 5), acc, false);
-    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(wi[1], 1.f, true),
-                                          __builtin_shufflevector(a, a, 6, 7), acc, false);
-    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(wi[2], 1.f, false),
-                                          __builtin_shufflevector(b, b, 0, 1), acc, false);
-    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(wi[2], 1.f, true),
-                                          __builtin_shufflevector(b, b, 2, 3), acc, false);
-    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(wi[3], 1.f, false),
-                                          __builtin_shufflevector(b, b, 4, 5), acc, false);
-    acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(wi[3], 1.f, true),
-                                          __builtin_shufflevector(b, b, 6, 7), acc, false);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(wb[0], __builtin_shufflevector(a, a, 0, 1), acc, false);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(wb[1], __builtin_shufflevector(a, a, 2, 3), acc, false);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(wb[2], __builtin_shufflevector(a, a, 4, 5), acc, false);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(wb[3], __builtin_shufflevector(a, a, 6, 7), acc, false);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(wb[4], __builtin_shufflevector(b, b, 0, 1), acc, false);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(wb[5], __builtin_shufflevector(b, b, 2, 3), acc, false);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(wb[6], __builtin_shufflevector(b, b, 4, 5), acc, false);
+    acc = __builtin_amdgcn_fdot2_f32_bf16(wb[7], __builtin_shufflevector(b, b, 6, 7), acc, false);
     return acc;
 }
 
@@ -197,14 +198,18 @@ __global__ void __launch_bounds__(256) gemv_kernel(const uint16_t* __restrict__ 
                 const int c = c0 + 4 * d;
                 if (c < nchunk) {
 #pragma unroll
-                    for (int r = 0; r < NR; ++r)
+                    for (int r = 0; r < NR; ++r) {
+                        if constexpr (WQ) {
+                            bf16x2_t wb[8];
+                            q2bf(wr[d][r], wb);
 #pragma unroll
-                        for (int m = 0; m < M; ++m) {
-                            if constexpr (WQ)
-                                acc[r * M + m] = qdot16(wr[d][r], xv[d][m][0], xv[d][m][1], acc[r * M + m]);
-                            else
-                                acc[r * M + m] = dot8(wr[d][r], xv[d][m][0], acc[r * M + m]);
+                            for (int m = 0; m < M; ++m)
+                                acc[r * M + m] = dot16(wb, xv[d][m][0], xv[d][m][1], acc[r * M + m]);
+                        } else {
+#pragma unroll
+                            for (int m = 0; m < M; ++m) acc[r * M + m] = dot8(wr[d][r], xv[d][m][0], acc[r * M + m]);
                         }
+                    }
                     if (c + 4 * DEPTH < nchunk) load(c + 4 * DEPTH, d);
                 }
             }
@@ -322,8 +327,10 @@ constexpr int rows_swiglu() { return M <= 2 ? 4 : 2; }
 
 // kResid rows per workgroup at M = 1: 4 (or 2 / 8 by knob) while the consumer's partial reduction (<= 2048 per row at
 // M = 1) still covers N / R, else 8.  The partials buffer is sized by gemv_resid_parts with the same choice.
-static int resid_rows(int N) {
-    const int r = knob("gemv_r_resid", 4);
+// fp8 weights (WQ): twice the rows per group — a group then streams the same bytes as the bf16 kernel's (at K = 4096
+// a wave holds a single 1 KiB chunk per row, so the per-group reduction / epilogue is amortised over 2x the rows)
+static int resid_rows(int N, bool wq = false) {
+    const int r = wq ? knob("gemv_q_r_resid", 8) : knob("gemv_r_resid", 4);
     if (r == 2 && N / 2 <= 2048 && N % 2 == 0) return 2;
     return (r == 4 && N / 4 <= 2048 && N % 4 == 0) ? 4 : 8;
 }
@@ -343,7 +350,10 @@ static int rows_knob(const char* name, int dflt) {
 template <int M, bool WQ = false>
 static void launch_m(const uint16_t* x, int mrows, int K, const uint16_t* W, int N, uint16_t* y, int mode,
                      const GemvNorm* nrm, const GemvRope* rp, hipStream_t st, const float* wscale = nullptr) {
-    constexpr int R1 = rows_plain<M>(), R2 = rows_swiglu<M>();
+    // WQ: twice the plain rows (O / down / QKV groups then stream the bf16 kernel's bytes); SwiGLU keeps its rows
+    // (gate_up at M = 1: 27.4 us with 4 + 4 rows, 35.9 with 8 + 8; profiles/r5/w8a16_*)
+    constexpr int R1 = rows_plain<M>() * (WQ ? 2 : 1), R2 = rows_swiglu<M>();
+    constexpr int RP = rows_plain<M>();  // kResid / M = 2 rope rows (the partials layout: gemv_resid_parts)
     const GemvNorm nz{};
     const GemvRope rz{};
     GemvNorm na = nrm ? *nrm : nz;
@@ -372,7 +382,7 @@ static void launch_m(const uint16_t* x, int mrows, int K, const uint16_t* W, int
     if (mode == kSwiglu) {
         const int F = N / 2;
         if constexpr (M == 1) {
-            const int r = rows_knob("gemv_r_swiglu", R2);
+            const int r = rows_knob(WQ ? "gemv_q_r_swiglu" : "gemv_r_swiglu", R2);
             if (r == 1) {
                 if (np) GV(kSwiglu, true, 1, F, F, F); else GV(kSwiglu, false, 1, F, F, F);
                 return;
@@ -390,7 +400,7 @@ static void launch_m(const uint16_t* x, int mrows, int K, const uint16_t* W, int
         else GV(kSwiglu, false, R2, F / R2, F, F);
     } else if (mode == kPlain) {
         if constexpr (M == 1) {
-            const int r = rows_knob("gemv_r_plain", R1);
+            const int r = rows_knob(WQ ? "gemv_q_r_plain" : "gemv_r_plain", R1);
             if (r == 2 && N % 2 == 0) {
                 if (np) GV(kPlain, true, 2, N / 2, N, 0); else GV(kPlain, false, 2, N / 2, N, 0);
                 return;
@@ -408,7 +418,7 @@ static void launch_m(const uint16_t* x, int mrows, int K, const uint16_t* W, int
         else GV(kPlain, false, R1, N / R1, N, 0);
     } else if constexpr (M <= 2) {
         if (mode == kResid) {
-            const int r = M == 1 ? resid_rows(N) : R1;
+            const int r = M == 1 ? resid_rows(N, WQ) : RP;
             if constexpr (M == 1) {
                 if (r == 4) {
                     GV(kResid, false, 4, N / 4, N, 0);
@@ -419,9 +429,9 @@ static void launch_m(const uint16_t* x, int mrows, int K, const uint16_t* W, int
                     return;
                 }
             }
-            GV(kResid, false, R1, N / R1, N, 0);
+            GV(kResid, false, RP, N / RP, N, 0);
         } else {
-            const int r = M == 1 ? rows_knob("gemv_r_rope", 4) : 8;
+            const int r = M == 1 ? rows_knob(WQ ? "gemv_q_r_rope" : "gemv_r_rope", WQ ? 8 : 4) : 8;
             if (mode == kRope) {
                 if (r == 4) {
                     if (np) GV(kRope, true, 4, N / 4, N, 0); else GV(kRope, false, 4, N / 4, N, 0);
@@ -467,7 +477,19 @@ void launch_gemv_ex(const uint16_t* x, int M, int K, const uint16_t* W, int N, u
     else launch_m<2>(x, M, K, W, N, y, mode, nrm, rope, st);
 }
 
-int gemv_resid_parts(int M, int N) { return N / (M == 1 ? resid_rows(N) : M <= 2 ? rows_plain<2>() : rows_plain<4>()); }
+int gemv_resid_parts(int M, int N, bool wq) {
+    return N / (M == 1 ? resid_rows(N, wq) : M <= 2 ? rows_plain<2>() : rows_plain<4>());
+}
+
+void launch_gemv_q(const uint16_t* x, int M, int K, const uint8_t* W, const float* wscale, int N, uint16_t* y,
+                   bool swiglu, hipStream_t st) {
+    if (M <= 0) return;
+    const uint16_t* w = reinterpret_cast<const uint16_t*>(W);
+    const int mode = swiglu ? kSwiglu : kPlain;
+    if (M == 1) launch_m<1, true>(x, M, K, w, N, y, mode, nullptr, nullptr, st, wscale);
+    else if (M == 2) launch_m<2, true>(x, M, K, w, N, y, mode, nullptr, nullptr, st, wscale);
+    else launch_m<4, true>(x, M, K, w, N, y, mode, nullptr, nullptr, st, wscale);
+}
 
 int launch_gemv_resid(const uint16_t* x, int M, int K, const uint16_t* W, int N, const uint16_t* rin, uint16_t* rout,
                       float* part_out, hipStream_t st, const float* wscale) {
@@ -481,7 +503,7 @@ int launch_gemv_resid(const uint16_t* x, int M, int K, const uint16_t* W, int N,
         else launch_m<2, true>(x, M, K, W, N, nullptr, kResid, &nrm, nullptr, st, wscale);
     } else if (M == 1) launch_m<1>(x, M, K, W, N, nullptr, kResid, &nrm, nullptr, st);
     else launch_m<2>(x, M, K, W, N, nullptr, kResid, &nrm, nullptr, st);
-    return gemv_resid_parts(M, N);
+    return gemv_resid_parts(M, N, wscale != nullptr);
 }
 
 }  // namespace chronos

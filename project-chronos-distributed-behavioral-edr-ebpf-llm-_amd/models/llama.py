@@ -29,8 +29,9 @@ from ..parallel.tp import TPContext
 # GEMV's prologue, RoPE + paged-KV write in the QKV GEMV's epilogue (CHRONOS_FUSE_NORM=0: the separate kernels)
 _FUSE_NORM = os.environ.get("CHRONOS_FUSE_NORM", "1") != "0"
 _FUSE_AR_NORM = os.environ.get("CHRONOS_FUSE_AR_NORM", "1") != "0"
-# fp8-weight decode (T <= 2): W8A16 GEMVs on bf16 activations with the bf16 path's fused epilogues (norm / RoPE + KV
-# write / residual) instead of W8A8 (an activation-quantisation launch per projection)
+# fp8-weight decode and jump-forward forwards (T <= 4): W8A16 GEMVs on bf16 activations (with the bf16 path's fused
+# norm / RoPE + KV write / residual epilogues at T <= 2) instead of W8A8 (an activation-quantisation launch per
+# projection)
 _W8A16_DECODE = os.environ.get("CHRONOS_W8A16_DECODE", "1") != "0"  # TP: fused IPC all-reduce + residual + RMSNorm
 # batched decode (>= 2048 (row, kv head) items, bf16 KV): RoPE + paged-KV write fused into the decode attention
 _FUSE_DECODE_ROPE = os.environ.get("CHRONOS_FUSE_DECODE_ROPE", "1") != "0"
@@ -490,6 +491,15 @@ class StepBatch:
     # decode rows: cascade attention over a shared prompt prefix (ops.decode_attention_rope ``casc``), device tensors
     # owned by the engine and updated in place between graph replays
     casc: Optional[tuple] = None
+    # a few tokens per sequence over long contexts (jump-forward forwards): (max tokens per sequence, kv splits) —
+    # the split-K decode kernel with all of a sequence's tokens in one pass over its K/V (ops.paged_attention
+    # max_q) instead of the prefill tiles, whose per-tile workgroups each stream the whole context
+    rows_dec: Optional[tuple] = None
+
+
+# decode-form attention for tiny chunks over long contexts (StepBatch.rows_dec): at least this much context (the
+# chunk's tokens per sequence x GQA group must fit the kernel's 16 query rows)
+ROWS_DEC_MIN_CTX = int(os.environ.get("CHRONOS_ROWS_DEC_MIN_CTX", "2048"))
 
 
 def make_prefill_batch(prompts: list[list[int]], starts: list[int], block_tables: list[list[int]], cfg: LlamaConfig,
@@ -530,6 +540,9 @@ def make_prefill_batch(prompts: list[list[int]], starts: list[int], block_tables
     it = lambda x: torch.tensor(x, dtype=torch.int32)  # noqa: E731
     sb = StepBatch(it(ids), it(pos), it(tok_seq), bt, it(qs), it(ctx), last,
                    torch.tensor(tiles, dtype=torch.int32).view(-1, 2), len(tiles), nqt, nsplit)
+    mq = max((len(t) for t in prompts), default=0)
+    if prompts and mq * (hq // hkv) <= 16 and max(ctx) >= ROWS_DEC_MIN_CTX and ctx_totals is None:
+        sb.rows_dec = (mq, ops.pick_nsplit(len(prompts) * hkv, max(ctx)))
     return to_device(sb, device)
 
 
@@ -546,7 +559,8 @@ def h2d(t: torch.Tensor | None, device) -> torch.Tensor | None:
 def to_device(sb: StepBatch, device) -> StepBatch:
     mv = lambda t: h2d(t, device)  # noqa: E731
     return StepBatch(mv(sb.ids), mv(sb.pos), mv(sb.tok_seq), mv(sb.block_table), mv(sb.q_start), mv(sb.ctx_len),
-                     mv(sb.last_idx), mv(sb.tiles), sb.ntiles, sb.nqt, sb.nsplit, sb.parts, sb.cp, sb.dec, sb.casc)
+                     mv(sb.last_idx), mv(sb.tiles), sb.ntiles, sb.nqt, sb.nsplit, sb.parts, sb.cp, sb.dec, sb.casc,
+                     sb.rows_dec)
 
 
 # -----------------------------------------------------------------------------------------------------------------
@@ -620,6 +634,11 @@ class LlamaModel:
             from ..parallel.context_parallel import ulysses_attention
 
             return ulysses_attention(q_buf, kv.k[li], kv.v[li], sb.cp, self.scale, kv.k_scale[li], kv.v_scale[li])
+        if attn is None and sb.rows_dec is not None and sb.cp is None:
+            mq, ns = sb.rows_dec  # every sequence's few tokens in one pass over its K/V
+            attn = ops.paged_attention(q_buf, kv.k[li], kv.v[li], sb.block_table, sb.q_start, sb.ctx_len, None,
+                                       sb.q_start.numel() - 1, 1, ns, self.scale, kv.k_scale[li], kv.v_scale[li],
+                                       max_q=mq)
         if attn is None:
             attn = ops.paged_attention(q_buf, kv.k[li], kv.v[li], sb.block_table, sb.q_start, sb.ctx_len, sb.tiles,
                                        sb.ntiles, sb.nqt, sb.nsplit, self.scale, kv.k_scale[li], kv.v_scale[li])
@@ -787,7 +806,7 @@ class LlamaModel:
             h = tp.all_reduce(ops.embedding(ids, w.embed, w.vocab_start))
             T = ids.numel()
             st = dict(sb=p, T=T, resid=h, q_buf=torch.empty(T, self.hq, cfg.head_dim, device=h.device, dtype=h.dtype),
-                      w16=(w.fp8 and _W8A16_DECODE and T <= 2 and h.is_cuda and p.cp is None and p.dec is None
+                      w16=(w.fp8 and _W8A16_DECODE and T <= 4 and h.is_cuda and p.cp is None and p.dec is None
                            and cfg.hidden_size % 1024 == 0))
             st["x"] = self._norm(h, st, w.layers[0].attn_norm, first=True)
             states.append(st)

@@ -207,11 +207,18 @@ def set_decode_gate(state: torch.Tensor | None, n: int = 0) -> None:
 
 def paged_attention(q, k_cache, v_cache, block_table, q_start, ctx_len, tiles=None, ntiles: int = 0, nqt: int = 1,
                     nsplit: int = 1, scale: float | None = None, k_scale: float = 1.0,
-                    v_scale: float = 1.0) -> torch.Tensor:
+                    v_scale: float = 1.0, max_q: int = 1) -> torch.Tensor:
+    """Paged attention: prefill tiles (``tiles``), decode rows (tiles None: token i is sequence i), or — tiles None,
+    ``max_q`` > 1 — sequences of up to max_q query tokens (q_start ranges, the last token at the end of its context)
+    in one pass over each sequence's K/V (split-K decode kernel; max_q x GQA group <= 16)."""
     scale = scale if scale is not None else 1.0 / math.sqrt(q.shape[-1])
     if _checking(q):
         nseq = ctx_len.shape[0] if tiles is None else q_start.shape[0] - 1
-        if tiles is None:
+        if tiles is None and max_q > 1:
+            qs = q_start.cpu().long()[:ntiles + 1]
+            _need(bool(((qs[1:] - qs[:-1]) <= max_q).all()) and int(qs[-1]) <= q.shape[0],
+                  "paged_attention: multi-token decode q_start")
+        elif tiles is None:
             _need(ntiles <= ctx_len.shape[0] and ntiles <= q.shape[0], "paged_attention: decode rows")
         else:
             tl = tiles.cpu().long()
@@ -221,9 +228,9 @@ def paged_attention(q, k_cache, v_cache, block_table, q_start, ctx_len, tiles=No
         _check_paged(block_table, k_cache, torch.arange(nseq), ctx_len[:nseq], "paged_attention")
     if q.is_cuda:
         return _k().paged_attention(q, k_cache, v_cache, block_table, q_start, ctx_len, tiles, ntiles, nqt, nsplit,
-                                    scale, k_scale, v_scale)
+                                    scale, k_scale, v_scale, max_q)
     return ref.paged_attention(q, k_cache, v_cache, block_table, q_start, ctx_len, tiles, ntiles, nqt, nsplit, scale,
-                               k_scale, v_scale)
+                               k_scale, v_scale, max_q)
 
 
 def decode_attention_rope(qkv, pos, cos_sin, k_cache, v_cache, block_table, ctx_len, n: int, hq: int,

@@ -251,9 +251,9 @@ def is_q(w) -> bool:
 
 
 def gemv_q_ok(m: int, n: int, k: int) -> bool:
-    """Shapes of the W8A16 decode GEMV (gemv.hip WQ: fp8 weights, bf16 activations): one or two rows, whole 1 KiB
-    weight chunks."""
-    return m <= 2 and k % 1024 == 0 and n % 16 == 0
+    """Shapes of the W8A16 decode GEMV (gemv.hip WQ: fp8 weights, bf16 activations): up to 4 rows (the fused
+    norm / RoPE / residual epilogues: 2), whole 1 KiB weight chunks."""
+    return m <= 4 and k % 1024 == 0 and n % 16 == 0
 
 
 def _q_fallback(x, w, swiglu: bool = False) -> torch.Tensor:
@@ -288,9 +288,9 @@ def resid_ok(m: int, n: int, k: int, fp8: bool = False) -> bool:
     """Shapes of the residual-epilogue producer: the M <= 2 GEMV shapes (gemv.hip kResid) and the batched GEMM's
     (gemm_pp.hip kResid) where the plan takes it; fp8 weights: the W8A16 GEMV shapes only."""
     if fp8:
-        return m <= GEMV_MAX_M and gemv_q_ok(m, n, k)
+        return m <= min(GEMV_MAX_M, 2) and gemv_q_ok(m, n, k)
     if m <= GEMV_MAX_M:
-        return gemv_ok(m, n, k)
+        return m <= 2 and gemv_ok(m, n, k)  # (the GEMV's residual epilogue: M <= 2)
     return pp_plan(m, n, k, PP_RESID) is not None
 
 
@@ -330,7 +330,7 @@ def gate_up_silu(x: torch.Tensor, w_gu: torch.Tensor) -> torch.Tensor:
 
     if is_q(w_gu):  # fp8 weights: the W8A16 GEMV (folded norm fused when x is a LazyNorm), else W8A8
         m, n, k = (x.rows() if isinstance(x, LazyNorm) else x.numel() // x.shape[-1]), w_gu.shape[0], x.shape[-1]
-        if isinstance(x, LazyNorm) and x.fusable() and gemv_q_ok(m, n, k):
+        if isinstance(x, LazyNorm) and x.fusable() and m <= 2 and gemv_q_ok(m, n, k):
             return _k().gemv_normp(x.s, x.part, x.eps, w_gu.q, True, w_gu.s)
         x = LazyNorm.force(x)
         if x.is_cuda and gemv_q_ok(m, n, k):
@@ -364,7 +364,7 @@ def linear(x, w: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tens
         from . import _k
 
         m, n, k = (x.rows() if isinstance(x, LazyNorm) else x.numel() // x.shape[-1]), w.shape[0], x.shape[-1]
-        if isinstance(x, LazyNorm) and x.fusable() and gemv_q_ok(m, n, k):
+        if isinstance(x, LazyNorm) and x.fusable() and m <= 2 and gemv_q_ok(m, n, k):
             return _k().gemv_normp(x.s, x.part, x.eps, w.q, False, w.s)
         x = LazyNorm.force(x)
         if x.is_cuda and gemv_q_ok(m, n, k):

@@ -119,15 +119,20 @@ def rope_kv_write(qkv, pos, tok_seq, block_table, cos_sin, q_out, k_cache, v_cac
 
 
 def paged_attention(q, k_cache, v_cache, block_table, q_start, ctx_len, tiles=None, ntiles=0, nqt=1, nsplit=1,
-                    scale: float | None = None, k_scale: float = 1.0, v_scale: float = 1.0) -> torch.Tensor:
-    """Causal varlen attention over the paged cache.  q [T, Hq, 128]; seqs given by q_start/ctx_len."""
+                    scale: float | None = None, k_scale: float = 1.0, v_scale: float = 1.0,
+                    max_q: int = 1) -> torch.Tensor:
+    """Causal varlen attention over the paged cache.  q [T, Hq, 128]; seqs given by q_start/ctx_len.  Decode mode
+    (tiles None): one token per sequence, or with max_q > 1 the q_start ranges (<= max_q tokens, the last at the end
+    of the context) — the same causal semantics as a prefill chunk."""
     T, hq, D = q.shape
     hkv, bs = k_cache.shape[1], k_cache.shape[2]
     G = hq // hkv
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     out = torch.zeros_like(q)
-    if tiles is None:  # decode: one token per sequence, seq i = token i
+    if tiles is None and max_q == 1:  # decode: one token per sequence, seq i = token i
         qs = list(range(ntiles + 1))
+    elif tiles is None:
+        qs = q_start[:ntiles + 1].tolist()
     else:
         qs = q_start.tolist()
     B = len(qs) - 1

@@ -35,7 +35,7 @@ from types import SimpleNamespace
 from typing import AsyncIterator, Optional
 
 
-def _worker(rank: int, cfg_dict: dict, req_q, res_q, device: str, fail_start: bool = False) -> None:
+def _worker(rank: int, cfg_dict: dict, req_q, res_q, device: str, fail_start: bool = False, replicas: int = 1) -> None:
     if fail_start:  # fault injection, set only through DPRouter(fault_start_ranks=...): die before ready
         print(f"[chronos router] replica {rank}: injected start-up fault (fault_start_ranks)", flush=True)
         raise SystemExit(7)
@@ -47,6 +47,8 @@ def _worker(rank: int, cfg_dict: dict, req_q, res_q, device: str, fail_start: bo
     if device == "cuda":
         torch.cuda.set_device(rank)
         cfg_dict = dict(cfg_dict, device=f"cuda:{rank}")
+    else:  # CPU replicas share the host: split its cores instead of each oversubscribing all of them
+        torch.set_num_threads(max(1, (os.cpu_count() or 1) // max(1, replicas)))
     eng = Engine(EngineConfig(**cfg_dict))
     res_q.put(("ready", rank, None))
 
@@ -94,6 +96,16 @@ def _worker(rank: int, cfg_dict: dict, req_q, res_q, device: str, fail_start: bo
         if eng.has_work():
             for r in eng.step():
                 live.pop(r.meta.get("rid"), None)
+
+
+def _deliver(loop, sink, kind, val) -> None:
+    """Hand a result to the caller's event loop; a caller whose loop has already closed (it gave up and returned) is
+    simply gone — not an error in the reader / supervisor thread."""
+    try:
+        loop.call_soon_threadsafe(sink, kind, val)
+    except RuntimeError:
+        if not loop.is_closed():
+            raise
 
 
 class DPRouter:
@@ -151,7 +163,7 @@ class DPRouter:
     def _spawn(self, r: int):
         self._ready_seen[r] = False
         p = self._ctx.Process(target=_worker, args=(r, self._cfgd, self._reqs[r], self._res, self._dev,
-                                                    r in self._fault_start), daemon=True)
+                                                    r in self._fault_start, self.n), daemon=True)
         p.start()
         return p
 
@@ -177,7 +189,7 @@ class DPRouter:
             if w is None:
                 continue
             loop, sink, _ = w
-            loop.call_soon_threadsafe(sink, kind, val)
+            _deliver(loop, sink, kind, val)
 
     def _error_result(self, r: int, msg: str) -> dict:
         now = time.perf_counter()
@@ -211,7 +223,7 @@ class DPRouter:
                     self.failed_requests += len(lost)
                 code = p.exitcode
                 for _, (loop, sink, _) in lost:  # answer at once: never leave a caller waiting for a dead replica
-                    loop.call_soon_threadsafe(sink, "done", self._error_result(r, f"replica {r} exited ({code})"))
+                    _deliver(loop, sink, "done", self._error_result(r, f"replica {r} exited ({code})"))
                 if self.respawn and not self._closing:
                     sf = self.start_failures[r]
                     if sf >= self.max_start_failures:

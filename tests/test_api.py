@@ -231,7 +231,7 @@ def test_dp_router_failover_and_respawn():
             ok_h, health = router.health()  # the fresh worker is still importing / building its engine
             done = []
             for t in tasks:
-                done.append(await asyncio.wait_for(t, 240))  # the survivor runs 400-token requests on CPU
+                done.append(await asyncio.wait_for(t, 600))  # the survivor runs 400-token requests on CPU
             failed = [i for i, d in enumerate(done) if d.done_reason == "error"]
             t_err = max(finished_at[i] for i in failed) - t_kill if failed else 99.0
             failed = [done[i] for i in failed]
@@ -247,7 +247,9 @@ def test_dp_router_failover_and_respawn():
 
         failed, t_err, ok_h, health, later, after = asyncio.run(go())
         assert failed and all("replica 0" in f.error for f in failed)
-        assert t_err < 1.0 + 0.5  # answered within ~1 s of the kill (poll 50 ms; replicas' CPU load adds jitter)
+        # answered promptly after the kill (poll 50 ms), not at the request's own end: the survivors' 400-token CPU
+        # decode takes far longer than this bound; CPU load from parallel test workers adds seconds of jitter
+        assert t_err < 4.0
         assert ok_h and health["status"] == "degraded" and 0 not in health["serving_replicas"]
         for o in later + after:
             assert o.done_reason == "stop" and set(json.loads(o.text)) == {"risk_score", "verdict", "reason"}

@@ -74,3 +74,33 @@ def test_split_lds_matches_reference(fp8, nb, ctx, nsplit):
         assert (o - want).abs().max().item() <= tol, (key, (o - want).abs().max().item(), tol)
     # in-launch combine == separate combine kernel (same merge code)
     assert torch.equal(outs[(1, 1)], outs[(1, 0)])
+
+
+@pytest.mark.parametrize("fp8", [False, True])
+@pytest.mark.parametrize("qlens,ctx,nsplit", [([3], [33000], 32), ([4, 1, 2], [8191, 100, 4097], 16),
+                                              ([2, 4], [700, 33], 4), ([4], [131072], 32), ([3, 3], [500, 37], 1)])
+def test_split_decode_multi_token(fp8, qlens, ctx, nsplit):
+    """Sequences of up to 4 query tokens (jump-forward chunks) in one pass over their K/V (max_q): against the fp32
+    reference of the same causal chunk attention, with the in-launch and the separate combine."""
+    from chronos import ops
+    from chronos.ops import reference as ref
+
+    hq, hkv = 32, 8
+    _, k, v, bt, _, cl = _case(ctx, hq, hkv, fp8, seed=sum(ctx) + sum(qlens))
+    T = sum(qlens)
+    q = torch.randn(T, hq, 128, device=DEV, generator=torch.Generator(device=DEV).manual_seed(T)).to(torch.bfloat16)
+    qs = torch.tensor([0] + list(torch.tensor(qlens).cumsum(0)), dtype=torch.int32, device=DEV)
+    ks, vs = (0.5, 0.25) if fp8 else (1.0, 1.0)
+    B, mq = len(ctx), max(qlens)
+    want = ref.paged_attention(q, k, v, bt, qs, cl, None, B, 1, nsplit, None, ks, vs, max_q=mq).float()
+    outs = {}
+    for comb in (1, 0):
+        torch.ops.chronos.set_knob("attn_inkernel_combine", comb)
+        torch.ops.chronos.set_knob("sd_inkernel_max_split", 1024 if comb else 4)
+        outs[comb] = ops.paged_attention(q, k, v, bt, qs, cl, None, B, 1, nsplit, None, ks, vs, max_q=mq).float()
+    torch.ops.chronos.set_knob("attn_inkernel_combine", 1)
+    torch.ops.chronos.set_knob("sd_inkernel_max_split", 4)
+    tol = 2e-2 * want.abs().max().item()
+    for comb, o in outs.items():
+        assert (o - want).abs().max().item() <= tol, (comb, (o - want).abs().max().item(), tol)
+    assert torch.equal(outs[1], outs[0])

@@ -35,7 +35,7 @@ def _close(y, want):
     assert err <= 1e-2 * want.float().abs().max().item() + 1e-3, (err, want.float().abs().max().item())
 
 
-@pytest.mark.parametrize("m", [1, 2])
+@pytest.mark.parametrize("m", [1, 2, 3, 4])
 @pytest.mark.parametrize("n,k,swiglu", [(6144, 4096, False), (4096, 14336, False), (28672, 4096, True),
                                         (4096, 4096, False), (512, 1024, True)])
 def test_gemv_w8a16(m, n, k, swiglu):
@@ -139,7 +139,12 @@ def test_fp8_model_decode_w8a16_vs_w8a8_and_bf16():
         dec = StepBatch(it([777]), it([61]), it([0]), bt_t, it([0, 1]), it([62]),
                         torch.zeros(1, dtype=torch.int64, device=DEV), None, 1)
         res[name] = m.forward(dec, kv).float()
+        # a jump-forward-sized prefill chunk (T = 3 tokens after the cached prompt): the unfused W8A16 GEMVs
+        jf = make_prefill_batch([[5, 6, 7]], [62], [bt], m.cfg, m.tp, DEV, max_blocks=8, nqt=2)
+        res[name + "_jf"] = m.forward(jf, kv).float()
     llama._W8A16_DECODE = True
     cos = lambda a, b: torch.nn.functional.cosine_similarity(a, b, dim=-1).min().item()  # noqa: E731
     assert cos(res["w8a16"], res["w8a8"]) > 0.995
     assert cos(res["w8a16"], res["bf16"]) > 0.98
+    assert cos(res["w8a16_jf"], res["w8a8_jf"]) > 0.995
+    assert cos(res["w8a16_jf"], res["bf16_jf"]) > 0.98
