@@ -29,9 +29,9 @@ from ..parallel.tp import TPContext
 # GEMV's prologue, RoPE + paged-KV write in the QKV GEMV's epilogue (CHRONOS_FUSE_NORM=0: the separate kernels)
 _FUSE_NORM = os.environ.get("CHRONOS_FUSE_NORM", "1") != "0"
 _FUSE_AR_NORM = os.environ.get("CHRONOS_FUSE_AR_NORM", "1") != "0"
-# fp8-weight decode and jump-forward forwards (T <= 4): W8A16 GEMVs on bf16 activations (with the bf16 path's fused
-# norm / RoPE + KV write / residual epilogues at T <= 2) instead of W8A8 (an activation-quantisation launch per
-# projection)
+# fp8-weight decode (T <= 2): W8A16 GEMVs on bf16 activations with the bf16 path's fused norm / RoPE + KV write /
+# residual epilogues instead of W8A8 (an activation-quantisation launch per projection).  Not at T = 3-4: the GEMV's
+# per-row-group overhead makes it slower there than the W8A8 GEMMs (gate_up 140 vs 27 us, profiles/r5/w8a16_*)
 _W8A16_DECODE = os.environ.get("CHRONOS_W8A16_DECODE", "1") != "0"  # TP: fused IPC all-reduce + residual + RMSNorm
 # batched decode (>= 2048 (row, kv head) items, bf16 KV): RoPE + paged-KV write fused into the decode attention
 _FUSE_DECODE_ROPE = os.environ.get("CHRONOS_FUSE_DECODE_ROPE", "1") != "0"
@@ -806,7 +806,7 @@ class LlamaModel:
             h = tp.all_reduce(ops.embedding(ids, w.embed, w.vocab_start))
             T = ids.numel()
             st = dict(sb=p, T=T, resid=h, q_buf=torch.empty(T, self.hq, cfg.head_dim, device=h.device, dtype=h.dtype),
-                      w16=(w.fp8 and _W8A16_DECODE and T <= 4 and h.is_cuda and p.cp is None and p.dec is None
+                      w16=(w.fp8 and _W8A16_DECODE and T <= 2 and h.is_cuda and p.cp is None and p.dec is None
                            and cfg.hidden_size % 1024 == 0))
             st["x"] = self._norm(h, st, w.layers[0].attn_norm, first=True)
             states.append(st)
