@@ -674,7 +674,9 @@ void lg_launch(const PPArgs& a, hipStream_t st) {
     X(74, 64, 32, 128, 4, 2)       \
     X(75, 128, 32, 128, 4, 2)      \
     X(76, 192, 128, 128, 3, 4)     \
-    X(77, 192, 128, 128, 3, 2)
+    X(77, 192, 128, 128, 3, 2)     \
+    X(78, 128, 32, 128, 7, 2)      \
+    X(79, 64, 32, 128, 12, 2)
 
 template <int MODE, bool NORMP>
 bool lg_mode(int cfg, const PPArgs& a, hipStream_t st) {

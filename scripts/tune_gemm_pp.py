@@ -105,9 +105,9 @@ def candidates(m, n, k, mode, keep=6):
                 if G._pp_valid(cfg, n, k, mode, sk) and (sk == 1 or (tiles < 256 and tiles * sk <= 1024)) \
                         and (cfg, sk) not in out:
                     out.append((cfg, sk))
-    # M <= 48: the same with 32-row x tiles (72-75)
-    if 2 <= m <= 48:
-        for cfg in (72, 73, 74, 75):
+    # M <= 48: the same with 32-row x tiles (72-75); to M = 256 the deep-ring ones (78-79: W bytes in flight)
+    if 2 <= m <= 256:
+        for cfg in ((72, 73, 74, 75, 78, 79) if m <= 48 else (73, 75, 78, 79)):
             bm, bn = G._PP_BM[cfg], G._PP_BN[cfg]
             tiles = -(-m // bm) * -(-n // bn)
             for sk in (1, 2, 4, 8):
