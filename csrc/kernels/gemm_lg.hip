@@ -120,6 +120,11 @@ __device__ __forceinline__ int lg_swz64(int row) { return (4 - ((row >> 2) & 3))
 template <int WN, int XM, int RB, int ST, int MODE, bool NORMP, int NWX, int ABL = 0, int VAR = 0, bool F8 = false>
 __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
     constexpr bool STG = VAR == 1, MAN = VAR == 2;
+    // VAR 3 (M32): the slab schedule on v_mfma_f32_32x32x16_bf16 — 32 x 32 blocks, half the MFMA issues per k-step
+    // for the same fragment reads (the 16x16x32 fragments of a wave are regrouped as 32-row blocks x two 16-deep k
+    // halves); the accumulators are copied into the 16x16 register order before split-K / the epilogue, which then
+    // maps (block, register) -> (n, m) with the 32x32 output layout
+    constexpr bool M32 = VAR == 3;
     constexpr int ES = F8 ? 1 : 2;  // operand bytes per element
     static_assert(!F8 || (ST >= 3 && RB == 128 && MODE != kResid && !NORMP && VAR == 0 && ABL == 0),
                   "fp8: ring schedule, 128-B rows, plain / SwiGLU epilogue");
@@ -141,6 +146,7 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
     constexpr bool SLAB = ST == 2;
     static_assert(!STG || (SLAB && NWX == 4), "staggered DMA: slab schedule, two waves per SIMD");
     static_assert(!MAN || SLAB, "issue-ordered k-steps: slab schedule");
+    static_assert(!M32 || (SLAB && !F8 && ABL == 0 && NT % 2 == 0 && MT % 2 == 0), "32x32 MFMA: slab schedule, bf16");
     static_assert(ST >= 3 || (SLAB && RB == 128), "slab schedule: 64-deep (128-B row) slabs");
     static_assert(MODE != kSwiglu || (WN / 4) % 16 == 0, "swiglu: WN/4 gate rows per wave, multiple of 16");
     static_assert(RB == 64 || RB == 128, "stage depth 32 or 64");
@@ -223,6 +229,17 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
             wrow0[s] = wi * (WN / 2) + 16 * s;
     }
     const int xrow0 = wj * (XM / NWX);
+    // M32: first W row of each 32-row block (SwiGLU: gate blocks, then the matching up blocks)
+    int wrow32[M32 ? NT / 2 : 1];
+    if constexpr (M32) {
+#pragma unroll
+        for (int S = 0; S < NT / 2; ++S) {
+            if constexpr (MODE == kSwiglu)
+                wrow32[S] = S < NT / 4 ? wi * (WN / 4) + 32 * S : WN / 2 + wi * (WN / 4) + 32 * (S - NT / 4);
+            else
+                wrow32[S] = wi * (WN / 2) + 32 * S;
+        }
+    }
     // F8: the two chunks 2 (lane >> 4) and 2 (lane >> 4) + 1 of the lane's 128-B row, swizzled like the bf16 reads
     int loff[F8 ? 2 : KS];
 #pragma unroll
@@ -286,14 +303,48 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
         auto rd = [&](int j, int kk, bf16x8 (&fa)[NT], bf16x8 (&fb)[MT]) {
             const unsigned char* wb = smem + (j & 1) * STAGE;
             const unsigned char* xb = wb + WIMG;
+            if constexpr (M32) {
+                // lane (r = lane & 31, h = lane >> 5): row r of the 32-row block, the 16-B chunk 2 k16 + h of the
+                // k-step's four (the same XOR swizzle by row & 7 as the 16x16 reads)
+                const int r = lane & 31;
+#pragma unroll
+                for (int k16 = 0; k16 < 2; ++k16) {
+                    const int co = (((4 * kk + 2 * k16 + (lane >> 5)) ^ (r & 7)) << 4);
+#pragma unroll
+                    for (int S = 0; S < NT / 2; ++S)
+                        fa[2 * S + k16] = *reinterpret_cast<const bf16x8*>(wb + (wrow32[S] + r) * RB + co);
+#pragma unroll
+                    for (int U = 0; U < MT / 2; ++U)
+                        fb[2 * U + k16] = *reinterpret_cast<const bf16x8*>(xb + (xrow0 + 32 * U + r) * RB + co);
+                }
+                return;
+            }
 #pragma unroll
             for (int s = 0; s < NT; ++s) fa[s] = *reinterpret_cast<const bf16x8*>(wb + wrow0[s] * RB + loff[kk]);
 #pragma unroll
             for (int t = 0; t < MT; ++t)
                 fb[t] = *reinterpret_cast<const bf16x8*>(xb + (xrow0 + 16 * t) * RB + loff[kk]);
         };
+        f32x16 acc32[M32 ? NT / 2 : 1][M32 ? MT / 2 : 1];
+        if constexpr (M32) {
+#pragma unroll
+            for (int S = 0; S < NT / 2; ++S)
+#pragma unroll
+                for (int U = 0; U < MT / 2; ++U)
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) acc32[S][U][i] = 0.f;
+        }
         auto mm = [&](bf16x8 (&fa)[NT], bf16x8 (&fb)[MT]) {
-            if constexpr (!(ABL & 4)) {
+            if constexpr (M32) {
+#pragma unroll
+                for (int k16 = 0; k16 < 2; ++k16)
+#pragma unroll
+                    for (int S = 0; S < NT / 2; ++S)
+#pragma unroll
+                        for (int U = 0; U < MT / 2; ++U)
+                            acc32[S][U] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[2 * S + k16], fb[2 * U + k16],
+                                                                                   acc32[S][U], 0, 0, 0);
+            } else if constexpr (!(ABL & 4)) {
 #pragma unroll
                 for (int s = 0; s < NT; ++s)
 #pragma unroll
@@ -306,7 +357,7 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
                 for (int i = 0; i < MT; ++i) asm volatile("" ::"v"(fb[i]));
             }
         };
-        constexpr int MF = NT * MT, NR = NT + MT;
+        constexpr int MF = M32 ? NT * MT / 2 : NT * MT, NR = NT + MT;
         if constexpr (STG) {
             if (grp == 0) lg_vmcnt<NPER>();  // slab 0 landed (group 0's part of slab 1 in flight)
             else lg_vmcnt<0>();
@@ -413,6 +464,18 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
             mm(fa1, fb1);
             lg_sched<0, MF, (ABL & 1) ? 0 : NPER, NR>();
             __builtin_amdgcn_sched_barrier(0);
+        }
+        if constexpr (M32) {
+            // 32x32 accumulator register 4 g + i -> acc[2 S + (g >> 1)][2 U + (g & 1)][i]
+#pragma unroll
+            for (int S = 0; S < NT / 2; ++S)
+#pragma unroll
+                for (int U = 0; U < MT / 2; ++U)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g)
+                        acc[2 * S + (g >> 1)][2 * U + (g & 1)] =
+                            f32x4{acc32[S][U][4 * g], acc32[S][U][4 * g + 1], acc32[S][U][4 * g + 2],
+                                  acc32[S][U][4 * g + 3]};
         }
     } else {
     // stage 0 landed for every wave (stages 1 .. ST-2 stay in flight)
@@ -555,6 +618,73 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
 
     // ---- epilogue: lane holds D[n = wrow0[s] + 4*(lane>>4) + i][m = xrow0 + 16*u + (lane&15)]
     const float* inv = reinterpret_cast<const float*>(smem + EXTRA + 16);
+    if constexpr (M32) {
+        // 32x32 layout: acc[s][2 U + gu] holds D[n = wrow32[s >> 1] + 8 g + 4 (lane >> 5) + i][m = xrow0 + 32 U +
+        // (lane & 31)], g = 2 (s & 1) + gu — both gu share the lane's row m, and lanes l, l ^ 32 the row's columns
+#pragma unroll
+        for (int U = 0; U < MT / 2; ++U) {
+            const int r = xrow0 + 32 * U + (lane & 31);
+            const int m = m0 + r;
+            float sc = 1.f;
+            if constexpr (NORMP) sc = inv[r];
+            float ss = 0.f;
+#pragma unroll
+            for (int gu = 0; gu < 2; ++gu) {
+                const int u = 2 * U + gu;
+                if constexpr (MODE == kSwiglu) {
+                    if (m < M) {
+#pragma unroll
+                        for (int s = 0; s < NT / 2; ++s) {
+                            const int g = 2 * (s & 1) + gu;
+                            const int f = tn * (WN / 2) + wrow32[s >> 1] + 8 * g + 4 * (lane >> 5);
+                            u16x4 o;
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) {
+                                const float gv = bf2f(f2bf(acc[s][u][i] * sc));
+                                const float sg = bf2f(f2bf(gv / (1.f + __expf(-gv))));
+                                o[i] = f2bf(sg * bf2f(f2bf(acc[s + NT / 2][u][i] * sc)));
+                            }
+                            *reinterpret_cast<u16x4*>(a.y + (int64_t)m * a.F + f) = o;
+                        }
+                    }
+                } else if constexpr (MODE == kResid) {
+                    if (m < M) {
+#pragma unroll
+                        for (int s = 0; s < NT; ++s) {
+                            const int g = 2 * (s & 1) + gu;
+                            const int n = tn * WN + wrow32[s >> 1] + 8 * g + 4 * (lane >> 5);
+                            const u16x4 rv = *reinterpret_cast<const u16x4*>(a.resid + (int64_t)m * a.N + n);
+                            u16x4 o;
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) {
+                                const float v = bf2f(f2bf(bf2f(f2bf(acc[s][u][i])) + bf2f(rv[i])));
+                                o[i] = f2bf(v);
+                                ss += v * v;
+                            }
+                            *reinterpret_cast<u16x4*>(a.y + (int64_t)m * a.N + n) = o;
+                        }
+                    }
+                } else {
+                    if (m < M) {
+#pragma unroll
+                        for (int s = 0; s < NT; ++s) {
+                            const int g = 2 * (s & 1) + gu;
+                            const int n = tn * WN + wrow32[s >> 1] + 8 * g + 4 * (lane >> 5);
+                            u16x4 o;
+#pragma unroll
+                            for (int i = 0; i < 4; ++i) o[i] = f2bf(acc[s][u][i] * sc);
+                            if (n < a.N) *reinterpret_cast<u16x4*>(a.y + (int64_t)m * a.N + n) = o;
+                        }
+                    }
+                }
+            }
+            if constexpr (MODE == kResid) {
+                ss += __shfl_xor(ss, 32, 64);
+                if (lane < 32 && m < M) a.part_out[(int64_t)m * (a.N / (WN / 2)) + tn * 2 + wi] = ss;
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int u = 0; u < MT; ++u) {
         const int r = xrow0 + 16 * u + (lane & 15);
@@ -676,7 +806,8 @@ void lg_launch(const PPArgs& a, hipStream_t st) {
     X(76, 192, 128, 128, 3, 4)     \
     X(77, 192, 128, 128, 3, 2)     \
     X(78, 128, 32, 128, 7, 2)      \
-    X(79, 64, 32, 128, 12, 2)
+    X(79, 64, 32, 128, 12, 2)      \
+    X(80, 256, 256, 128, 2, 4, 3)
 
 template <int MODE, bool NORMP>
 bool lg_mode(int cfg, const PPArgs& a, hipStream_t st) {

@@ -86,7 +86,7 @@ def candidates(m, n, k, mode, keep=6):
     # (from M = 128: the wide-W-row tiles over the whole x panel, split-K to fill the chip — at mid-M the L2 -> LDS
     # feed, not HBM, bounds the stream, and x bytes per workgroup scale with x rows / W rows)
     if m >= 128:
-        for cfg in (20, 29, 30, 19, 31, 23, 76, 77, 22):
+        for cfg in (20, 80, 29, 30, 19, 31, 23, 76, 77, 22):
             bm, bn = G._PP_BM[cfg], G._PP_BN[cfg]
             tiles = -(-m // bm) * -(-n // bn)
             for sk in (1, 2, 4):

@@ -36,7 +36,7 @@ def _check(y, ref, tol=2e-2):
 
 
 LG = [12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 34, 35, 36, 37, 38, 39, 72, 73, 74, 75, 78,
-      79]
+      79, 80]
 # gemm_lg.hip configs (12-19 / 29-31 ring schedule, 20-28 slab schedule, 32-39 mid-M weight streaming); 76-77 (192 W
 # rows: plain epilogue only at these toy N, whose SwiGLU / residual widths are not multiples of 192)
 LG192 = [76, 77]
