@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--num-predict", type=int, default=64)
     ap.add_argument("--single-stream", type=int, default=16, help="chains for the single-stream p50 latency")
     ap.add_argument("--burst", type=int, default=8)
+    ap.add_argument("--small-burst", type=int, default=2,
+                    help="decode steps per burst for a bucket of <= 2 rows (the single-stream phase; 0 = --burst)")
     ap.add_argument("--tail-burst", type=int, default=4,
                     help="decode steps per burst once a >=128-row bucket has started to drain (0 = always --burst)")
     ap.add_argument("--no-graphs", action="store_true")
@@ -200,6 +202,7 @@ def main():
             tp.enable_ipc_allreduce()
     cfg = EngineConfig(model=a.model, device=str(device), max_slots=a.streams, max_model_len=a.max_model_len,
                        default_num_predict=a.num_predict, decode_burst=a.burst, tail_burst=a.tail_burst,
+                       small_burst=a.small_burst,
                        use_graphs=not a.no_graphs,
                        prefix_cache=not a.no_prefix_cache, partial_prefix=not a.no_partial_prefix,
                        async_harvest=a.async_harvest, seed=0,

@@ -62,13 +62,14 @@ def main():
         for k, v in knobsets.get(name, {}).items():
             if k == "py_split_max":  # decode kv-split cap (ops.pick_nsplit), baked into the captured graph
                 ops._SPLIT_MAX = v
-            elif k in ("py_burst", "py_jump", "py_gemv_max_m"):  # engine decode_burst / jump_forward / GEMV routing
+            elif k in ("py_burst", "py_jump", "py_gemv_max_m", "py_small_burst"):  # engine decode_burst / jump_forward / GEMV routing
                 pass
             else:
                 torch.ops.chronos.set_knob(k, v)  # read when this engine's decode graph is captured
         llama._FUSE_NORM = fuse
         burst = knobsets.get(name, {}).get("py_burst", a.burst)
         eng = Engine(EngineConfig(model=a.model, device="cuda", max_slots=8, max_model_len=512, decode_burst=burst,
+                                  small_burst=knobsets.get(name, {}).get("py_small_burst", 0),
                                   decode_gate=gate, seed=0, async_harvest=a.async_harvest, weight_dtype=a.weights,
                                   jump_forward=bool(knobsets.get(name, {}).get("py_jump", 1))))
         # capture the n=1 graph under this variant's setting
