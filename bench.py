@@ -51,7 +51,7 @@ def parse():
     ap.add_argument("--num-predict", type=int, default=64)
     ap.add_argument("--single-stream", type=int, default=16, help="chains for the single-stream p50 latency")
     ap.add_argument("--burst", type=int, default=8)
-    ap.add_argument("--small-burst", type=int, default=2,
+    ap.add_argument("--small-burst", type=int, default=1,
                     help="decode steps per burst for a bucket of <= 2 rows (the single-stream phase; 0 = --burst)")
     ap.add_argument("--tail-burst", type=int, default=4,
                     help="decode steps per burst once a >=128-row bucket has started to drain (0 = always --burst)")

@@ -80,8 +80,8 @@ class EngineConfig:
     # Decode buckets of at most small_burst_rows rows (one or two sensor streams in flight) run bursts of small_burst
     # steps: the steps a burst runs after its row closed its verdict or parked on a grammar-forced run are gated but
     # not free, and the host harvest between bursts is cheap at this size (single stream, 24 chains: 2.85 ms/token at
-    # 8 steps, 2.75 at 4, 2.73 at 2; profiles/r5/single_stream_burst_ab*.json).  0 disables.
-    small_burst: int = 2
+    # 8 steps, 2.75 at 4, 2.73 at 2, 2.72 at 1; profiles/r5/single_stream_burst_ab*.json).  0 disables.
+    small_burst: int = 1
     small_burst_rows: int = 2
     use_graphs: bool = True
     grammar_capacity: int = 2048
