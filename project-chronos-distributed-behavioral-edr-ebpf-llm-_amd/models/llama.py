@@ -785,7 +785,8 @@ class LlamaModel:
         if (tp.world > 1 and sb.tiles is not None and self.sequence_parallel and not w.fp8 and sb.cp is None
                 and sb.dec is None):
             return self._forward_sp(sb, kv, logits_dtype)
-        if (0 < self.decode_overlap_rows <= sb.ntiles and sb.tiles is None and sb.dec is None and sb.cp is None
+        if (0 < self.decode_overlap_rows and max(2, self.decode_overlap_rows) <= sb.ntiles and sb.tiles is None
+                and sb.dec is None and sb.cp is None
                 and tp.world > 1 and tp.fast_allreduce_norm is not None and not w.fp8 and _FUSE_AR_NORM
                 and self.device.type == "cuda"):
             return self._forward_dec_overlap(sb, kv, logits_dtype)

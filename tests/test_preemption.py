@@ -93,3 +93,20 @@ def test_auto_reservation_picks_by_pool_size():
     lazy growth + preemption when it does not."""
     assert _engine(kv_alloc="auto").kv_alloc == "full"
     assert _engine(kv_alloc="auto", kv_blocks=40).kv_alloc == "lazy"
+
+
+def test_small_bucket_bursts_match_full_bursts():
+    """EngineConfig.small_burst (1-step bursts for buckets of <= 2 rows, the single-stream regime) changes only when
+    the host harvests, never the tokens: greedy verdicts equal the 4-step-burst engine's, chain after chain."""
+    chains = synthetic_chains(4, seed=8, native=False)
+    outs = []
+    for sb in (0, 1):
+        eng = _engine(kv_alloc="full", small_burst=sb, jump_forward=True)
+        got = []
+        for c in chains:  # one chain in flight at a time
+            r = eng.submit(build_prompt(c.history), fmt=VERDICT_SCHEMA, num_predict=40)
+            eng.run_until_idle()
+            assert r.done_reason in ("stop", "length")
+            got.append(r.out_ids)
+        outs.append(got)
+    assert outs[0] == outs[1]
