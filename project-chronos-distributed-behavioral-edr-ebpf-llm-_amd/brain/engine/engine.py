@@ -928,9 +928,11 @@ class Engine:
                                self.s_nout[:n], self.s_out[:n], self.s_topk[:n], self.s_topp[:n], self._jump_flags(n))
 
     def _jump_flags(self, rows: int):
-        """The sampler's park-on-forced-run flags for a decode batch of ``rows`` sequences (None = never park).  Not
-        with async harvest: its snapshots lag one burst, so a row already jumped would still read as parked."""
-        if self.cfg.jump_forward and not self._async and self.bank.jumps and 0 < rows <= self.cfg.jump_max_rows:
+        """The sampler's park-on-forced-run flags for a decode batch of ``rows`` sequences (None = never park).  With
+        async harvest the snapshot a row parked in is read one burst late: the burst launched meanwhile runs that row
+        gated (the sampler leaves parked rows untouched), the jump's device writes queue behind it, and the next
+        snapshot — taken before the jump — is recognised as stale by the row's ``jump_seq`` (``_harvest``)."""
+        if self.cfg.jump_forward and self.bank.jumps and 0 < rows <= self.cfg.jump_max_rows:
             return self.bank.jump
         return None
 

@@ -115,14 +115,21 @@ def test_no_jump_forward_also_teacher_forced(tok):
 
 
 @pytest.mark.gpu
-def test_jump_forward_gpu_graphs_teacher_forced():
+@pytest.mark.parametrize("asy", [False, True])
+def test_jump_forward_gpu_graphs_teacher_forced(asy):
     """GPU engine, captured decode bursts, parking in the HIP sampler: the same properties as on the CPU (bf16 decode
-    vs prefill rounding: looser tie tolerance)."""
+    vs prefill rounding: looser tie tolerance); also with async harvest (single chains and a batch)."""
     from chronos.brain.engine.engine import Engine, EngineConfig
     from chronos.sensor.prompt import VERDICT_SCHEMA
 
-    eng = Engine(EngineConfig(model="small", device="cuda", max_slots=4, max_model_len=256, decode_burst=4))
-    reqs = [eng.submit(p, fmt=VERDICT_SCHEMA, num_predict=48) for p in _prompts()]
+    eng = Engine(EngineConfig(model="small", device="cuda", max_slots=4, max_model_len=256, decode_burst=4,
+                              async_harvest=asy))
+    reqs = []
+    if asy:  # one chain at a time first (1-step bursts, the single-stream regime)
+        for p in _prompts(2):
+            reqs.append(eng.submit(p, fmt=VERDICT_SCHEMA, num_predict=48))
+            eng.run_until_idle()
+    reqs += [eng.submit(p, fmt=VERDICT_SCHEMA, num_predict=48) for p in _prompts()]
     eng.run_until_idle()
     assert eng.stats["jumps"] > 0
     for r in reqs:
@@ -215,3 +222,32 @@ def test_sampler_greedy_on_padded_logits_view():
     ops.constrained_sample(logits, None, nxt, dist, -5, state, rem, torch.zeros(n, device="cuda"), i32([0] * n),
                            i32([0] * n), i32([0] * n), i32([1] * n), i32([0] * n), out)
     assert out[:, 0].tolist() == logits.float().argmax(1).tolist()
+
+
+@pytest.mark.parametrize("burst", [1, 4])
+def test_jump_forward_with_async_harvest_teacher_forced(tok, burst):
+    """Async harvest (burst k harvested while burst k+1 runs) with jump-forward: a parked row is seen one burst late,
+    the stale snapshot taken before its jump is skipped, and every verdict is still the teacher-forced greedy one —
+    the same tokens as the synchronous engine, one chain at a time and several in flight."""
+    from chronos.brain.engine.engine import Engine, EngineConfig
+    from chronos.sensor.prompt import VERDICT_SCHEMA
+
+    outs = {}
+    for asy in (False, True):
+        eng = Engine(EngineConfig(model="tiny", device="cpu", max_slots=4, max_model_len=384, use_graphs=False,
+                                  decode_burst=burst, small_burst=0, max_prefill_tokens=128, jump_forward=True,
+                                  async_harvest=asy), tokenizer=tok)
+        single = []
+        for p in _prompts(2):
+            r = eng.submit(p, fmt=VERDICT_SCHEMA, num_predict=40)
+            eng.run_until_idle()
+            single.append(r)
+        batch = [eng.submit(p, fmt=VERDICT_SCHEMA, num_predict=40) for p in _prompts(3)]
+        eng.run_until_idle()
+        for r in single + batch:
+            json.loads(r.text)
+            _teacher_forced_ok(eng, r)
+        assert eng.stats["jumps"] > 0
+        assert eng.blocks.free == eng.blocks.num_blocks - 1 and not eng.running
+        outs[asy] = [r.out_ids for r in single + batch]
+    assert outs[True] == outs[False]
