@@ -26,6 +26,9 @@ SHAPES = {
     # residual add follows the all-reduce)
     "70b-tp8": {"qkv": (1280, 8192, 0), "o": (8192, 1024, 0), "gate_up": (7168, 8192, 1), "down": (8192, 3584, 0),
                 "lm_head": (16032, 8192, 0)},
+    # Llama-3-70B on one GPU (141 GB of bf16 weights in HBM): TP = 1 shapes, residual epilogues on O / down
+    "70b": {"qkv": (10240, 8192, 0), "o": (8192, 8192, 2), "gate_up": (57344, 8192, 1), "down": (8192, 28672, 2),
+            "lm_head": (128256, 8192, 0)},
 }
 MS = [1, 2, 3, 4, 5, 8, 16, 32, 48, 64, 128, 256, 512, 768, 1024, 2048, 4096, 8192, 16384]
 
