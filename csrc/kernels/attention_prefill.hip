@@ -578,6 +578,278 @@ __global__ void __launch_bounds__(256, 2) attn_prefill2_kernel(
         }
 }
 
+// ------------------------------------------------------------------------------------------------------------------
+// v8: fp8 KV cache on the block-scaled fp8 MFMA (BASELINE.json config "128k-token kill-chain context window, paged KV +
+// CDNA4 fp8 MFMA").  Same tiling as v2 LEAN (4 waves x 32 query rows, 64 keys per stage, S^T = K Q^T with the score
+// tile reused in registers as the P operand), but both products run on v_mfma_scale_f32_32x32x64_f8f6f4 with unit MX
+// scales: 4x the K of the bf16 32x32x16 in 2x its cycles, so a stage is 8 MFMAs (4 QK^T + 4 PV) instead of 32.
+// PMC on v2 LEAN fp8 (profiles/r5/prefill_pmc_v2_fp8.txt): 8.1 VALU per MFMA, issue-bound — the 32 per-stage fp8 -> bf16
+// conversions of K and V and 24 of the 32 MFMA issue slots are what this variant removes; K / V stay e4m3 from HBM to
+// the MFMA.
+//   * Q: each row is quantised once in the prologue to e4m3 with its own scale (amax / 448 over the 128 dims, the lane
+//     pair lane / lane ^ 32 holds one row); that scale, k_scale and softmax_scale * log2(e) form one per-lane score
+//     multiplier, applied to the row max and fused into the exponent's fma as in v2 LEAN.
+//   * P: the exp'd scores (<= 2^kRescaleThr = 256 < 448 under the deferred max) are packed to e4m3 (v_cvt_pk_fp8_f32,
+//     16 per stage, as many as v2's bf16 packs); row sums stay f32.  v_scale folds into the output normalisation.
+//   * fragments: lane l of the f8f6f4 MFMA holds 32 k-bytes of row / column l & 31 for lane half l >> 5, the same
+//     (half, byte) -> k map for A and B, so any k permutation shared by both operands is exact.  QK^T: byte j of half
+//     hf = head dim 64c + 32hf + j (MFMA c = 0, 1).  PV: byte j of half hf = key (j >> 4) * 32 + 8 ((j >> 2) & 3) +
+//     4 hf + (j & 3) — exactly the keys the lane's S^T accumulators hold (registers 16 kb + i of S^T block kb) — so
+//     the V^T image stores each dim row's 64 keys in that order and every operand is two conflict-free ds_read_b128.
+//   * LDS per stage: K [64 keys][128 B] with the 16-B chunk c of key k at slot c ^ ((k >> 1) & 7) (the 16 lanes of a
+//     ds_read_b128 group cover both row parities x 8 slots); V^T [128 dims][64 key bytes] at an 80-B pitch.  18 KiB per
+//     stage, two stages, register-staged (T14 split) with one barrier per stage.
+// Accuracy: Q and P take one more e4m3 rounding each, the rounding the cache already applies to K and V
+// (tests/test_prefill_fp8_mfma_gpu.py checks against the fp32 reference on the dequantised cache).
+// ------------------------------------------------------------------------------------------------------------------
+constexpr int kK8Img = 64 * 128;
+constexpr int kV8Pitch = 80;
+constexpr int kV8Img = 128 * kV8Pitch;
+template <bool PV8>
+constexpr int stage8_bytes() { return kK8Img + (PV8 ? kV8Img : kV2Img); }
+
+// PV8 = false: only Q K^T on the fp8 MFMA; V is converted to bf16 at staging and P.V runs on the bf16 32x32x16 MFMA
+// exactly as in v2 LEAN (the P operand keeps bf16 precision) — the accuracy / speed middle point (knob value 2).
+template <bool PV8>
+__global__ void __launch_bounds__(256, 2) attn_prefill8_kernel(
+    const uint16_t* __restrict__ q, const uint8_t* __restrict__ kc, const uint8_t* __restrict__ vc,
+    const int32_t* __restrict__ block_table, int bt_stride, const int32_t* __restrict__ q_start,
+    const int32_t* __restrict__ ctx_len, const int32_t* __restrict__ tiles, int ntiles, uint16_t* __restrict__ out,
+    int hq, int hkv, float scale_log2, float k_scale, float v_scale) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    typedef float f32x16_t __attribute__((ext_vector_type(16)));
+    typedef int i32x8_t __attribute__((ext_vector_type(8)));
+    typedef int i32x4_t __attribute__((ext_vector_type(4)));
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int col = lane & 31, hf = lane >> 5;
+    const int G = hq / hkv;
+    const int h = blockIdx.y;
+    const int tile = ntiles - 1 - (int)blockIdx.x;  // heaviest first
+    const int seq = tiles[2 * tile], rel0 = tiles[2 * tile + 1];
+    const int qbase = q_start[seq], qlen = q_start[seq + 1] - qbase;
+    const int ctx = ctx_len[seq], ctx0 = ctx - qlen;
+    const int32_t* bt = block_table + (int64_t)seq * bt_stride;
+
+    // ---- this lane's query row, quantised: dims 64c + 32hf + j in byte j of qf[c] ----
+    const int R = w * 32 + col;
+    const int tr = rel0 + R / G, hd = h * G + R % G;
+    const bool rvalid = tr < qlen;
+    const int rpos = rvalid ? ctx0 + tr : -1;
+    i32x8_t qf[2];
+    float cl;  // score multiplier: q scale * k_scale * softmax scale * log2(e)
+    {
+        const uint16_t* qp = q + ((int64_t)(qbase + (rvalid ? tr : 0)) * hq + hd) * kPD + 32 * hf;
+        u16x8 raw[8];
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) raw[4 * c + j] = *reinterpret_cast<const u16x8*>(qp + 64 * c + 8 * j);
+        float amax = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(bf2f(raw[i][e])));
+        amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
+        if (!rvalid) amax = 0.f;
+        const float inv = amax > 0.f ? kFp8Max / amax : 0.f;  // invalid / all-zero row: every byte 0
+        cl = (amax > 0.f ? amax / kFp8Max : 1.f) * k_scale * scale_log2;
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+#pragma unroll
+            for (int d = 0; d < 8; ++d) {
+                const u16x8& v = raw[4 * c + (d >> 1)];
+                const int o = 4 * (d & 1);
+                qf[c][d] = (int)f32x4_to_fp8x4(bf2f(v[o]) * inv, bf2f(v[o + 1]) * inv, bf2f(v[o + 2]) * inv,
+                                               bf2f(v[o + 3]) * inv);
+            }
+    }
+    int last_tr = rel0 + 128 / G - 1;
+    if (last_tr > qlen - 1) last_tr = qlen - 1;
+    const int kv_end = ctx0 + last_tr + 1;
+    const int nsteps = (kv_end + 63) >> 6;
+    const int wave_min_pos = ctx0 + rel0 + (w * 32) / G;
+
+    // ---- staging (block_size 16, checked by the launcher): K 32 B of one key per thread, V^T 2 pages x 16 B of one
+    // dim row per thread; addresses = one 64-bit block base + a per-thread constant (v2 LEAN) ----
+    const int kkey = threadIdx.x >> 2, kq = threadIdx.x & 3;
+    const int vdim = threadIdx.x >> 1, vh = threadIdx.x & 1;
+    const int64_t blk_el = (int64_t)hkv * 16 * kPD;  // bytes per cache block
+    const int nblk_m1 = (kv_end + 15) / 16 - 1;
+    const int koffc = (h * 16 + (kkey & 15)) * kPD + kq * 32;
+    const int voffc = (h * kPD + vdim) * 16;
+    const int kpg = kkey >> 4, vpg = vh * 2;
+    constexpr int kStage8 = stage8_bytes<PV8>();
+    uint4 ks[2], vs[2];
+    auto gload = [&](int s) {
+        const int64_t kblk = bt[min(s * 4 + kpg, nblk_m1)];
+        const uint4* kp = reinterpret_cast<const uint4*>(kc + kblk * blk_el + koffc);
+        ks[0] = kp[0];
+        ks[1] = kp[1];
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            const int64_t vblk = bt[min(s * 4 + vpg + b, nblk_m1)];
+            vs[b] = *reinterpret_cast<const uint4*>(vc + vblk * blk_el + voffc);
+        }
+    };
+    auto swrite = [&](int buf, int s) {
+        if (s * 64 + 64 > kv_end) {  // the stage reaching past kv_end: zero keys / pages past it (wave-uniform)
+            if (s * 64 + kkey >= kv_end) ks[0] = ks[1] = uint4{0u, 0u, 0u, 0u};
+#pragma unroll
+            for (int b = 0; b < 2; ++b)
+                if (s * 64 + vh * 32 + b * 16 >= kv_end) vs[b] = uint4{0u, 0u, 0u, 0u};
+        }
+        unsigned char* base = lds + buf * kStage8;
+        const int sw = (kkey >> 1) & 7;
+        *reinterpret_cast<uint4*>(base + kkey * 128 + (((2 * kq) ^ sw) << 4)) = ks[0];
+        *reinterpret_cast<uint4*>(base + kkey * 128 + (((2 * kq + 1) ^ sw) << 4)) = ks[1];
+        if constexpr (PV8) {
+            // page b word wd = keys vh*32 + 16b + 4wd + 0..3 -> half wd & 1, dword 2b + (wd >> 1) of 16-B block vh
+            unsigned char* vr = base + kK8Img + vdim * kV8Pitch + vh * 16;
+            *reinterpret_cast<uint4*>(vr) = uint4{vs[0].x, vs[0].z, vs[1].x, vs[1].z};
+            *reinterpret_cast<uint4*>(vr + 32) = uint4{vs[0].y, vs[0].w, vs[1].y, vs[1].w};
+        } else {  // v2's bf16 V^T image: keys of every 16-key group in the P operand's k order
+            unsigned char* vr = base + kK8Img + vdim * kV2Pitch + vh * 64;
+#pragma unroll
+            for (int b = 0; b < 2; ++b) {
+                const u16x8 lo = __builtin_bit_cast(u16x8, fp8x8_to_bf16x8_raw(vs[b].x, vs[b].y));
+                const u16x8 hi = __builtin_bit_cast(u16x8, fp8x8_to_bf16x8_raw(vs[b].z, vs[b].w));
+                *reinterpret_cast<u16x4*>(vr + 32 * b) = u16x4{lo[0], lo[1], lo[2], lo[3]};
+                *reinterpret_cast<u16x4*>(vr + 32 * b + 16) = u16x4{lo[4], lo[5], lo[6], lo[7]};
+                *reinterpret_cast<u16x4*>(vr + 32 * b + 8) = u16x4{hi[0], hi[1], hi[2], hi[3]};
+                *reinterpret_cast<u16x4*>(vr + 32 * b + 24) = u16x4{hi[4], hi[5], hi[6], hi[7]};
+            }
+        }
+    };
+
+    float m = -1e30f, lsum = 0.f;
+    f32x16_t o[4];
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[db][i] = 0.f;
+
+    if (nsteps > 0) {
+        gload(0);
+        swrite(0, 0);
+    }
+    const bool wave_invalid = __any(rpos < 0);
+    __syncthreads();
+    for (int s = 0; s < nsteps; ++s) {
+        if (s + 1 < nsteps) gload(s + 1);  // in flight under this stage's MFMAs
+        const unsigned char* base = lds + (s & 1) * kStage8;
+        const int t0 = s * 64;
+        // ---- S^T for the stage's two 32-key blocks: 2 fp8 MFMAs each ----
+        f32x16_t sc[2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            f32x16_t acc;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+            const int row = kb * 32 + col;
+            const int sw = (row >> 1) & 7;
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const int u = 4 * c + 2 * hf;
+                const i32x4_t lo = *reinterpret_cast<const i32x4_t*>(base + row * 128 + ((u ^ sw) << 4));
+                const i32x4_t hi = *reinterpret_cast<const i32x4_t*>(base + row * 128 + (((u + 1) ^ sw) << 4));
+                const i32x8_t kf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+                acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(kf, qf[c], acc, 0, 0, 0, 127, 0, 127);
+            }
+            sc[kb] = acc;
+        }
+        // ---- online softmax (v2 LEAN with the per-lane multiplier cl) ----
+        const bool edge = (t0 + 64 > kv_end) || (t0 + 63 > wave_min_pos) || wave_invalid;
+        if (edge) {
+            const int lim = min(kv_end, rpos + 1) - (t0 + 4 * hf);
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int i = 0; i < 16; ++i)
+                    sc[kb][i] = (kb * 32 + (i & 3) + 8 * (i >> 2)) >= lim ? -INFINITY : sc[kb][i];
+        }
+        float mx = -INFINITY;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sc[kb][i]);
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * cl;
+        if (__any(mx > m + kRescaleThr)) {
+            const float mnew = fmaxf(m, mx);
+            const float alpha = __builtin_amdgcn_exp2f(m - mnew);
+            m = mnew;
+            lsum *= alpha;
+#pragma unroll
+            for (int db = 0; db < 4; ++db) o[db] *= alpha;
+        }
+        float ps = 0.f;
+        const float nm = -m;
+        if constexpr (PV8) {
+            i32x8_t pf;
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int i = 0; i < 16; i += 4) {
+                    float p[4];
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        p[e] = __builtin_amdgcn_exp2f(fmaf(sc[kb][i + e], cl, nm));
+                        ps += p[e];
+                    }
+                    int r = __builtin_amdgcn_cvt_pk_fp8_f32(p[0], p[1], 0, false);
+                    pf[kb * 4 + (i >> 2)] = __builtin_amdgcn_cvt_pk_fp8_f32(p[2], p[3], r, true);
+                }
+            // ---- O^T += V^T . P^T: one fp8 MFMA per 32-dim block ----
+#pragma unroll
+            for (int db = 0; db < 4; ++db) {
+                const unsigned char* vr = base + kK8Img + (db * 32 + col) * kV8Pitch + hf * 32;
+                const i32x4_t lo = *reinterpret_cast<const i32x4_t*>(vr);
+                const i32x4_t hi = *reinterpret_cast<const i32x4_t*>(vr + 16);
+                const i32x8_t vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+                o[db] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf, pf, o[db], 0, 0, 0, 127, 0, 127);
+            }
+        } else {
+            bf16x8 pf[2][2];
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    const float p = __builtin_amdgcn_exp2f(fmaf(sc[kb][i], cl, nm));
+                    ps += p;
+                    pf[kb][i >> 3][i & 7] = (__bf16)p;
+                }
+#pragma unroll
+            for (int db = 0; db < 4; ++db) {
+                const unsigned char* vr = base + kK8Img + (db * 32 + col) * kV2Pitch;
+#pragma unroll
+                for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2) {
+                        const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vr + 2 * (kb * 32 + 16 * s2 + 8 * hf));
+                        o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kb][s2], o[db], 0, 0, 0);
+                    }
+            }
+        }
+        lsum += ps;
+        if (s + 1 < nsteps) swrite((s + 1) & 1, s + 1);
+        __syncthreads();
+    }
+
+    // ---- epilogue: lane holds O^T[dims 32 db + 8 g + 4 hf + (0..3)][its row] ----
+    const float lt = lsum + __shfl_xor(lsum, 32, 64);
+    if (!rvalid) return;
+    const float inv = (lt > 0.f ? 1.f / lt : 0.f) * v_scale;
+    uint16_t* op = out + ((int64_t)(qbase + tr) * hq + hd) * kPD + 4 * hf;
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            u16x4 v;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = f2bf(o[db][4 * g + i] * inv);
+            *reinterpret_cast<u16x4*>(op + 32 * db + 8 * g) = v;
+        }
+}
+
 void launch_attn_prefill(const uint16_t* q, const void* kc, const void* vc, const int32_t* block_table,
                          int bt_stride, const int32_t* q_start, const int32_t* ctx_len, const int32_t* tiles,
                          int ntiles, uint16_t* out, int hq, int hkv, int block_size, float scale, bool fp8,
@@ -585,6 +857,28 @@ void launch_attn_prefill(const uint16_t* q, const void* kc, const void* vc, cons
     if (ntiles == 0) return;
     // 2 (default): v2 LEAN; 5: v2 as before LEAN (kept for in-process A/B); 0 / 1: the 32-key-step kernel
     const int variant = knob("prefill_variant", 2);
+    const int f8 = fp8 && variant == 2 && block_size == 16 ? knob("prefill_fp8_mfma", 1) : 0;
+    if (f8 == 1 || f8 == 2) {  // 1: Q K^T and P V on the fp8 MFMA; 2: Q K^T only
+        static bool attr8 = hipFuncSetAttribute((const void*)attn_prefill8_kernel<true>,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                2 * stage8_bytes<true>()) == hipSuccess &&
+                            hipFuncSetAttribute((const void*)attn_prefill8_kernel<false>,
+                                                hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                2 * stage8_bytes<false>()) == hipSuccess;
+        (void)attr8;
+        const float sl2 = scale * 1.4426950408889634f;
+        const uint8_t* k8 = static_cast<const uint8_t*>(kc);
+        const uint8_t* v8 = static_cast<const uint8_t*>(vc);
+        if (f8 == 1)
+            hipLaunchKernelGGL(attn_prefill8_kernel<true>, dim3(ntiles, hkv), dim3(256), 2 * stage8_bytes<true>(), st,
+                               q, k8, v8, block_table, bt_stride, q_start, ctx_len, tiles, ntiles, out, hq, hkv, sl2,
+                               k_scale, v_scale);
+        else
+            hipLaunchKernelGGL(attn_prefill8_kernel<false>, dim3(ntiles, hkv), dim3(256), 2 * stage8_bytes<false>(),
+                               st, q, k8, v8, block_table, bt_stride, q_start, ctx_len, tiles, ntiles, out, hq, hkv,
+                               sl2, k_scale, v_scale);
+        return;
+    }
     if (variant == 2 || variant == 5) {
         static bool attr2 = [] {
             bool ok = true;

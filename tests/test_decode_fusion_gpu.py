@@ -338,11 +338,13 @@ def test_flash_prefill_forced_rescale(variant, spike, kv):
     spike="big": the stage max beats the running one by far more than v2's deferred-max threshold (8 in log2 units),
     so the rescale branch runs.  spike="small": it rises by ~3-4 log2 units, below the threshold, so v2 keeps the
     stale max and accumulates p up to 2^8 (cdna_hip_programming.md §5.4 rule 26).  kv="fp8" runs the same branches
-    in attn_prefill2_kernel<true> on dequantised e4m3 scores."""
+    in attn_prefill2_kernel<true> on dequantised e4m3 scores; the fp8-MFMA kernel that is the default
+    for an fp8 cache has its own copy of this test (tests/test_prefill_fp8_mfma_gpu.py)."""
     from chronos import ops
     from chronos.ops import reference as ref
 
     torch.ops.chronos.set_knob("prefill_variant", variant)
+    torch.ops.chronos.set_knob("prefill_fp8_mfma", 0)
     try:
         g = torch.Generator(device=DEV).manual_seed(123 + variant)
         hq, hkv, bs = 32, 8, 16
@@ -371,3 +373,4 @@ def test_flash_prefill_forced_rescale(variant, spike, kv):
         assert bool((d <= 2e-2 + 2e-2 * exp.float().abs()).all()), float(d.max())
     finally:
         torch.ops.chronos.set_knob("prefill_variant", 2)
+        torch.ops.chronos.set_knob("prefill_fp8_mfma", 1)

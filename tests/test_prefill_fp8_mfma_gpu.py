@@ -1,0 +1,149 @@
+"""fp8-MFMA flash prefill (attention_prefill.hip attn_prefill8_kernel: Q and P quantised to e4m3, both products on
+v_mfma_scale_f32_32x32x64_f8f6f4) against the fp32 reference on the dequantised e4m3 cache, and against the bf16-MFMA
+kernel it replaces (knob prefill_fp8_mfma=0) on the same inputs.
+
+Ragged sequences with cached prefixes (chunked prefill), GQA groups of 4 (Llama-3-8B) and 8 (70B), tail tiles, the
+forced-rescale path, and the long-context chunk shape the 128k config runs."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _case(g, q_lens, prefix, hq, hkv, ks=0.25, vs=0.5, bs=16, kamp=1.0, with_bf16=False):
+    from chronos import ops
+    from chronos.ops import reference as ref
+
+    ctx = [p + n for p, n in zip(prefix, q_lens)]
+    nbs = [(c + bs - 1) // bs for c in ctx]
+    nb = sum(nbs) + 1
+    k = (torch.randn(nb, hkv, bs, 128, device=DEV, generator=g) * kamp).to(torch.bfloat16)
+    v = torch.randn(nb, hkv, 128, bs, device=DEV, generator=g).to(torch.bfloat16)
+    bt = torch.zeros(len(q_lens), max(nbs), dtype=torch.int32)
+    o = 1
+    for b, n in enumerate(nbs):
+        bt[b, :n] = torch.arange(o, o + n, dtype=torch.int32)
+        o += n
+    T = sum(q_lens)
+    q = torch.randn(T, hq, 128, device=DEV, generator=g).to(torch.bfloat16)
+    qs = [0]
+    for n in q_lens:
+        qs.append(qs[-1] + n)
+    tiles = ops.attention_tiles(q_lens, hq, hkv, 8)
+    tt = torch.tensor(tiles, dtype=torch.int32, device=DEV).view(-1, 2)
+    k8, v8 = ref.to_fp8_bytes(k, 1 / ks), ref.to_fp8_bytes(v, 1 / vs)
+    args = (q, k8, v8, bt.to(DEV), torch.tensor(qs, dtype=torch.int32, device=DEV),
+            torch.tensor(ctx, dtype=torch.int32, device=DEV), tt, len(tiles), 8, 1, None, ks, vs)
+    if with_bf16:  # the same attention on the bf16 cache the e4m3 bytes were quantised from
+        return args, (q, k, v) + args[3:11] + (1.0, 1.0)
+    return args
+
+
+def _run(args, fp8_mfma):
+    from chronos import ops
+
+    ops.load()
+    torch.ops.chronos.set_knob("prefill_fp8_mfma", fp8_mfma)
+    try:
+        return ops.paged_attention(*args)
+    finally:
+        torch.ops.chronos.set_knob("prefill_fp8_mfma", 1)
+
+
+def _errs(out, exp):
+    d = (out.float() - exp.float())
+    return float(d.norm() / exp.float().norm()), float(d.abs().max())
+
+
+@pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8)])
+@pytest.mark.parametrize("shape", ["ragged", "prefix"])
+def test_fp8_mfma_prefill_vs_fp32(hq, hkv, shape):
+    from chronos.ops import reference as ref
+
+    g = torch.Generator(device=DEV).manual_seed(hq + len(shape))
+    if shape == "ragged":
+        q_lens, prefix = [1, 37, 200, 513], [0, 5, 300, 0]
+    else:
+        q_lens, prefix = [700, 64], [2000, 4100]
+    args, args16 = _case(g, q_lens, prefix, hq, hkv, with_bf16=True)
+    exp = ref.paged_attention(*args)
+    truth = ref.paged_attention(*args16)  # fp32 attention on the unquantised bf16 cache
+    out8 = _run(args, 1)
+    outqk = _run(args, 2)
+    out16 = _run(args, 0)
+    rel8, max8 = _errs(out8, exp)
+    relqk, maxqk = _errs(outqk, exp)
+    rel16, max16 = _errs(out16, exp)
+    print(f"fp8-MFMA rel {rel8:.4f} max {max8:.4f} | QK-only rel {relqk:.4f} max {maxqk:.4f} | "
+          f"bf16-MFMA rel {rel16:.4f} max {max16:.4f}")
+    # against the bf16-cache truth: what the e4m3 cache alone costs vs what the fp8 MFMA adds on top
+    t16, t8, tqk = _errs(out16, truth)[0], _errs(out8, truth)[0], _errs(outqk, truth)[0]
+    print(f"vs bf16-cache truth: fp8 cache + bf16-MFMA {t16:.4f} | fp8-MFMA {t8:.4f} | QK-only {tqk:.4f}")
+    assert torch.isfinite(out8).all() and torch.isfinite(outqk).all()
+    assert rel16 < 0.01
+    assert relqk < 0.035, (relqk, rel16)
+    assert rel8 < 0.05, (rel8, rel16)
+    assert max8 < 0.25, max8
+    # measured r5: the e4m3 cache alone 3.5-3.9 % rel; + fp8 MFMA 4.5-5.4 %; + fp8 Q K^T only 4.1-4.7 %
+    assert t8 < 1.6 * t16 and tqk < 1.35 * t16, (t8, tqk, t16)
+
+
+def test_fp8_mfma_prefill_long_chunk():
+    """A 4k chunk over a 28k prefix (the long-context chunk shape, scaled to fit the fp32 reference)."""
+    from chronos.ops import reference as ref
+
+    g = torch.Generator(device=DEV).manual_seed(7)
+    args = _case(g, [4096], [28672], 32, 8)
+    out8 = _run(args, 1)
+    exp = ref.paged_attention(*args)
+    rel8, max8 = _errs(out8, exp)
+    print(f"long chunk fp8-MFMA rel {rel8:.4f} max {max8:.4f}")
+    assert torch.isfinite(out8).all()
+    assert rel8 < 0.05 and max8 < 0.25, (rel8, max8)
+
+
+@pytest.mark.parametrize("spike", ["big", "small"])
+def test_fp8_mfma_prefill_forced_rescale(spike):
+    """Late keys aligned with one query row push the stage max past the running max by ~14 (big: rescale branch) or
+    ~3.5 (small: deferred max, p up to 2^8 packed to e4m3) log2 units."""
+    from chronos import ops
+    from chronos.ops import reference as ref
+
+    g = torch.Generator(device=DEV).manual_seed(11)
+    hq, hkv, bs = 32, 8, 16
+    ks, vs = 0.25, 0.5
+    q_lens, prefix = [1200], [900]
+    nb = (2100 + bs - 1) // bs + 1
+    k = (torch.randn(nb, hkv, bs, 128, device=DEV, generator=g) * 0.3).to(torch.bfloat16)
+    v = torch.randn(nb, hkv, 128, bs, device=DEV, generator=g).to(torch.bfloat16)
+    q = torch.randn(1200, hq, 128, device=DEV, generator=g).to(torch.bfloat16)
+    amp = 0.9 if spike == "big" else 0.25
+    for t in range(1500, 1564):
+        k[1 + t // bs, 3, t % bs] = (q[t - 900, 12].float() * amp).to(torch.bfloat16)
+    k8, v8 = ref.to_fp8_bytes(k, 1 / ks), ref.to_fp8_bytes(v, 1 / vs)
+    bt = torch.arange(1, nb, dtype=torch.int32, device=DEV).view(1, -1)
+    tiles = ops.attention_tiles(q_lens, hq, hkv, 8)
+    tt = torch.tensor(tiles, dtype=torch.int32, device=DEV).view(-1, 2)
+    args = (q, k8, v8, bt, torch.tensor([0, 1200], dtype=torch.int32, device=DEV),
+            torch.tensor([2100], dtype=torch.int32, device=DEV), tt, len(tiles), 8, 1, None, ks, vs)
+    out8 = _run(args, 1)
+    exp = ref.paged_attention(*args)
+    rel8, max8 = _errs(out8, exp)
+    print(f"rescale {spike}: fp8-MFMA rel {rel8:.4f} max {max8:.4f}")
+    assert torch.isfinite(out8).all()
+    assert rel8 < 0.05 and max8 < 0.25, (rel8, max8)
+
+
+def test_fp8_mfma_prefill_zero_query_rows():
+    """All-zero query rows (quantisation scale 0 -> unit scale) give the uniform average of the visible values."""
+    from chronos.ops import reference as ref
+
+    g = torch.Generator(device=DEV).manual_seed(3)
+    args = list(_case(g, [96], [40], 32, 8))
+    args[0] = args[0].clone()
+    args[0][10:20] = 0
+    out8 = _run(tuple(args), 1)
+    exp = ref.paged_attention(*args)
+    rel8, max8 = _errs(out8[10:20], exp[10:20])
+    assert rel8 < 0.05 and max8 < 0.1, (rel8, max8)
