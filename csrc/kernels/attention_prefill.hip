@@ -610,7 +610,19 @@ constexpr int stage8_bytes() { return kK8Img + (PV8 ? kV8Img : kV2Img); }
 
 // PV8 = false: only Q K^T on the fp8 MFMA; V is converted to bf16 at staging and P.V runs on the bf16 32x32x16 MFMA
 // exactly as in v2 LEAN (the P operand keeps bf16 precision) — the accuracy / speed middle point (knob value 2).
-template <bool PV8>
+// FOLD (knob values 1, 2; 3 = PV8 without it, for A/B): with 8 MFMAs a stage the kernel is VALU-issue-bound, so the
+// per-score VALU goes into the MFMAs —
+//   * k_scale * softmax_scale * log2(e) multiplies Q before quantisation and the row's quantisation scale is a power
+//     of two fed to the MFMA's own E8M0 scale operand (per lane = per query row), so S^T comes out in log2 units;
+//   * the QK^T accumulators start from -m (a 16-register copy of the running max, C != D), so p = v_exp_f32(S^T)
+//     directly: no per-score fma.  m starts at the first stage's row max (set, not rescaled, at s = 0);
+//   * (PV8) row sums come from one more fp8 MFMA against an all-ones A operand (e4m3 1.0 = 0x38): the sum of the
+//     e4m3 P the P.V product used, instead of 32 v_add_f32 per stage.
+// Measured and not kept: two stages of register lookahead (loads for s + 2 issued at the top of s into a second
+// register set): 1640 vs 1632 TFLOP/s, within noise — the kernel is not load-latency-bound at one stage
+// (profiles/r5/prefill_fp8_mfma_depth_ab.jsonl).
+// MSUM (PV8 only): the row sums from the all-ones fp8 MFMA (part of FOLD, separable for A/B).
+template <bool PV8, bool FOLD, bool MSUM>
 __global__ void __launch_bounds__(256, 2) attn_prefill8_kernel(
     const uint16_t* __restrict__ q, const uint8_t* __restrict__ kc, const uint8_t* __restrict__ vc,
     const int32_t* __restrict__ block_table, int bt_stride, const int32_t* __restrict__ q_start,
@@ -636,7 +648,8 @@ __global__ void __launch_bounds__(256, 2) attn_prefill8_kernel(
     const bool rvalid = tr < qlen;
     const int rpos = rvalid ? ctx0 + tr : -1;
     i32x8_t qf[2];
-    float cl;  // score multiplier: q scale * k_scale * softmax scale * log2(e)
+    float cl;      // score multiplier: q scale * k_scale * softmax scale * log2(e) (not FOLD)
+    int qe = 127;  // FOLD: E8M0 scale of this row's e4m3 Q
     {
         const uint16_t* qp = q + ((int64_t)(qbase + (rvalid ? tr : 0)) * hq + hd) * kPD + 32 * hf;
         u16x8 raw[8];
@@ -651,8 +664,21 @@ __global__ void __launch_bounds__(256, 2) attn_prefill8_kernel(
             for (int e = 0; e < 8; ++e) amax = fmaxf(amax, fabsf(bf2f(raw[i][e])));
         amax = fmaxf(amax, __shfl_xor(amax, 32, 64));
         if (!rvalid) amax = 0.f;
-        const float inv = amax > 0.f ? kFp8Max / amax : 0.f;  // invalid / all-zero row: every byte 0
-        cl = (amax > 0.f ? amax / kFp8Max : 1.f) * k_scale * scale_log2;
+        float inv;
+        if constexpr (FOLD) {
+            const float sl = k_scale * scale_log2;
+            int e = 0;
+            if (amax > 0.f) {
+                (void)frexpf(amax * sl / kFp8Max, &e);  // 2^e >= amax * sl / 448
+                e = min(max(e, -126), 126);
+            }
+            inv = amax > 0.f ? ldexpf(sl, -e) : 0.f;
+            qe = e + 127;
+            cl = 1.f;
+        } else {
+            inv = amax > 0.f ? kFp8Max / amax : 0.f;  // invalid / all-zero row: every byte 0
+            cl = (amax > 0.f ? amax / kFp8Max : 1.f) * k_scale * scale_log2;
+        }
 #pragma unroll
         for (int c = 0; c < 2; ++c)
 #pragma unroll
@@ -721,12 +747,18 @@ __global__ void __launch_bounds__(256, 2) attn_prefill8_kernel(
         }
     };
 
-    float m = -1e30f, lsum = 0.f;
-    f32x16_t o[4];
+    float m = FOLD ? 0.f : -1e30f, lsum = 0.f;
+    f32x16_t o[4], negm, lacc;
 #pragma unroll
     for (int db = 0; db < 4; ++db)
 #pragma unroll
         for (int i = 0; i < 16; ++i) o[db][i] = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) negm[i] = lacc[i] = 0.f;
+    constexpr bool kMfmaSum = PV8 && MSUM;
+    i32x8_t pf8 = {0, 0, 0, 0, 0, 0, 0, 0};  // e4m3 P; persists so each pack's first half merges into a live register
+    const i32x8_t ones = {0x38383838, 0x38383838, 0x38383838, 0x38383838,
+                          0x38383838, 0x38383838, 0x38383838, 0x38383838};
 
     if (nsteps > 0) {
         gload(0);
@@ -743,8 +775,12 @@ __global__ void __launch_bounds__(256, 2) attn_prefill8_kernel(
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
             f32x16_t acc;
+            if constexpr (FOLD) {
+                acc = negm;
+            } else {
 #pragma unroll
-            for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+                for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+            }
             const int row = kb * 32 + col;
             const int sw = (row >> 1) & 7;
 #pragma unroll
@@ -753,7 +789,7 @@ __global__ void __launch_bounds__(256, 2) attn_prefill8_kernel(
                 const i32x4_t lo = *reinterpret_cast<const i32x4_t*>(base + row * 128 + ((u ^ sw) << 4));
                 const i32x4_t hi = *reinterpret_cast<const i32x4_t*>(base + row * 128 + (((u + 1) ^ sw) << 4));
                 const i32x8_t kf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-                acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(kf, qf[c], acc, 0, 0, 0, 127, 0, 127);
+                acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(kf, qf[c], acc, 0, 0, 0, 127, 0, qe);
             }
             sc[kb] = acc;
         }
@@ -773,7 +809,25 @@ __global__ void __launch_bounds__(256, 2) attn_prefill8_kernel(
 #pragma unroll
             for (int i = 0; i < 16; ++i) mx = fmaxf(mx, sc[kb][i]);
         mx = fmaxf(mx, __shfl_xor(mx, 32, 64)) * cl;
-        if (__any(mx > m + kRescaleThr)) {
+        if constexpr (FOLD) {
+            // mx is relative to m (the accumulators started at -m)
+            if (s == 0 || __any(mx > kRescaleThr)) {
+                float d = s == 0 ? mx : fmaxf(mx, 0.f);
+                if (!(d > -INFINITY)) d = 0.f;  // every key masked (invalid row): keep m
+                if (s > 0) {
+                    const float alpha = __builtin_amdgcn_exp2f(-d);
+                    lsum *= alpha;
+                    lacc *= alpha;
+#pragma unroll
+                    for (int db = 0; db < 4; ++db) o[db] *= alpha;
+                }
+                m += d;
+#pragma unroll
+                for (int kb = 0; kb < 2; ++kb) sc[kb] -= d;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) negm[i] = -m;
+            }
+        } else if (__any(mx > m + kRescaleThr)) {
             const float mnew = fmaxf(m, mx);
             const float alpha = __builtin_amdgcn_exp2f(m - mnew);
             m = mnew;
@@ -783,8 +837,11 @@ __global__ void __launch_bounds__(256, 2) attn_prefill8_kernel(
         }
         float ps = 0.f;
         const float nm = -m;
+        auto expo = [&](float x) {
+            return FOLD ? __builtin_amdgcn_exp2f(x) : __builtin_amdgcn_exp2f(fmaf(x, cl, nm));
+        };
         if constexpr (PV8) {
-            i32x8_t pf;
+            i32x8_t& pf = pf8;
 #pragma unroll
             for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
@@ -792,10 +849,10 @@ __global__ void __launch_bounds__(256, 2) attn_prefill8_kernel(
                     float p[4];
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
-                        p[e] = __builtin_amdgcn_exp2f(fmaf(sc[kb][i + e], cl, nm));
-                        ps += p[e];
+                        p[e] = expo(sc[kb][i + e]);
+                        if constexpr (!kMfmaSum) ps += p[e];
                     }
-                    int r = __builtin_amdgcn_cvt_pk_fp8_f32(p[0], p[1], 0, false);
+                    const int r = __builtin_amdgcn_cvt_pk_fp8_f32(p[0], p[1], pf[kb * 4 + (i >> 2)], false);
                     pf[kb * 4 + (i >> 2)] = __builtin_amdgcn_cvt_pk_fp8_f32(p[2], p[3], r, true);
                 }
             // ---- O^T += V^T . P^T: one fp8 MFMA per 32-dim block ----
@@ -807,13 +864,15 @@ __global__ void __launch_bounds__(256, 2) attn_prefill8_kernel(
                 const i32x8_t vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
                 o[db] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf, pf, o[db], 0, 0, 0, 127, 0, 127);
             }
+            if constexpr (kMfmaSum) lacc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ones, pf, lacc, 0, 0, 0, 127,
+                                                                                           0, 127);
         } else {
             bf16x8 pf[2][2];
 #pragma unroll
             for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
                 for (int i = 0; i < 16; ++i) {
-                    const float p = __builtin_amdgcn_exp2f(fmaf(sc[kb][i], cl, nm));
+                    const float p = expo(sc[kb][i]);
                     ps += p;
                     pf[kb][i >> 3][i & 7] = (__bf16)p;
                 }
@@ -835,7 +894,7 @@ __global__ void __launch_bounds__(256, 2) attn_prefill8_kernel(
     }
 
     // ---- epilogue: lane holds O^T[dims 32 db + 8 g + 4 hf + (0..3)][its row] ----
-    const float lt = lsum + __shfl_xor(lsum, 32, 64);
+    const float lt = kMfmaSum ? lacc[0] : lsum + __shfl_xor(lsum, 32, 64);
     if (!rvalid) return;
     const float inv = (lt > 0.f ? 1.f / lt : 0.f) * v_scale;
     uint16_t* op = out + ((int64_t)(qbase + tr) * hq + hd) * kPD + 4 * hf;
@@ -858,25 +917,37 @@ void launch_attn_prefill(const uint16_t* q, const void* kc, const void* vc, cons
     // 2 (default): v2 LEAN; 5: v2 as before LEAN (kept for in-process A/B); 0 / 1: the 32-key-step kernel
     const int variant = knob("prefill_variant", 2);
     const int f8 = fp8 && variant == 2 && block_size == 16 ? knob("prefill_fp8_mfma", 1) : 0;
-    if (f8 == 1 || f8 == 2) {  // 1: Q K^T and P V on the fp8 MFMA; 2: Q K^T only
-        static bool attr8 = hipFuncSetAttribute((const void*)attn_prefill8_kernel<true>,
-                                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                2 * stage8_bytes<true>()) == hipSuccess &&
-                            hipFuncSetAttribute((const void*)attn_prefill8_kernel<false>,
-                                                hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                2 * stage8_bytes<false>()) == hipSuccess;
+    // 1: Q K^T and P V on the fp8 MFMA; 2: Q K^T only (FOLD); 3: 1 with FOLD; 4: 2 without.  FOLD measured neutral to
+    // negative with P V on the fp8 MFMA (1605 vs 1638 TFLOP/s on the 112k-prefix chunk, its 9th MFMA and the -m copies
+    // cost what the removed VALU saved) and +3.8 % for Q K^T only (profiles/r5/prefill_fp8_mfma_fold_ab.jsonl)
+    if (f8 >= 1 && f8 <= 5) {  // 5: 1 with the MFMA row sums only
+        static bool attr8 = [] {
+            bool ok = true;
+            for (const void* f : {(const void*)attn_prefill8_kernel<true, true, true>,
+                                  (const void*)attn_prefill8_kernel<true, false, false>,
+                                  (const void*)attn_prefill8_kernel<true, false, true>})
+                ok &= hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * stage8_bytes<true>()) ==
+                      hipSuccess;
+            for (const void* f : {(const void*)attn_prefill8_kernel<false, true, false>,
+                                  (const void*)attn_prefill8_kernel<false, false, false>})
+                ok &= hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * stage8_bytes<false>()) ==
+                      hipSuccess;
+            return ok;
+        }();
         (void)attr8;
         const float sl2 = scale * 1.4426950408889634f;
         const uint8_t* k8 = static_cast<const uint8_t*>(kc);
         const uint8_t* v8 = static_cast<const uint8_t*>(vc);
-        if (f8 == 1)
-            hipLaunchKernelGGL(attn_prefill8_kernel<true>, dim3(ntiles, hkv), dim3(256), 2 * stage8_bytes<true>(), st,
-                               q, k8, v8, block_table, bt_stride, q_start, ctx_len, tiles, ntiles, out, hq, hkv, sl2,
-                               k_scale, v_scale);
-        else
-            hipLaunchKernelGGL(attn_prefill8_kernel<false>, dim3(ntiles, hkv), dim3(256), 2 * stage8_bytes<false>(),
-                               st, q, k8, v8, block_table, bt_stride, q_start, ctx_len, tiles, ntiles, out, hq, hkv,
-                               sl2, k_scale, v_scale);
+#define AP8_LAUNCH(PV, FO, MS)                                                                                    \
+    hipLaunchKernelGGL((attn_prefill8_kernel<PV, FO, MS>), dim3(ntiles, hkv), dim3(256), 2 * stage8_bytes<PV>(), st, q, \
+                       k8, v8, block_table, bt_stride, q_start, ctx_len, tiles, ntiles, out, hq, hkv, sl2, k_scale,    \
+                       v_scale)
+        if (f8 == 1) AP8_LAUNCH(true, false, false);
+        else if (f8 == 2) AP8_LAUNCH(false, true, false);
+        else if (f8 == 3) AP8_LAUNCH(true, true, true);
+        else if (f8 == 5) AP8_LAUNCH(true, false, true);
+        else AP8_LAUNCH(false, false, false);
+#undef AP8_LAUNCH
         return;
     }
     if (variant == 2 || variant == 5) {

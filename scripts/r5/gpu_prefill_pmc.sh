@@ -2,7 +2,8 @@
 # r5: flash prefill (attn_prefill2, fp8 KV, 16k chunk over a 112k prefix): timing, then two PMC passes
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-O=gpurun_out/r5ppmc
+O=${PMC_OUT:-gpurun_out/r5ppmc}
+export PMC_OUT=$O
 mkdir -p $O
 timeout -k 10 200 python -u scripts/bench_prefill_attn.py --variants 2 --cases chunk16k_prefix112k,chunk16k_prefix0 > $O/t_bf16.log 2>&1 || { tail -20 $O/t_bf16.log; exit 1; }
 grep '^{' $O/t_bf16.log
@@ -18,7 +19,7 @@ for P in "$P1" "$P2"; do
 done
 python3 - <<'PY'
 import csv, glob, collections
-for f in sorted(glob.glob("gpurun_out/r5ppmc/p*/**/*counter_collection.csv", recursive=True)):
+for f in sorted(glob.glob(""+__import__("os").environ.get("PMC_OUT","gpurun_out/r5ppmc")+"/p*/**/*counter_collection.csv", recursive=True)):
     agg = collections.defaultdict(float); n = collections.Counter()
     for r in csv.DictReader(open(f)):
         if "attn_prefill" not in r.get("Kernel_Name", ""):
