@@ -622,12 +622,13 @@ constexpr int stage8_bytes() { return kK8Img + (PV8 ? kV8Img : kV2Img); }
 // register set): 1640 vs 1632 TFLOP/s, within noise — the kernel is not load-latency-bound at one stage
 // (profiles/r5/prefill_fp8_mfma_depth_ab.jsonl).
 // MSUM (PV8 only): the row sums from the all-ones fp8 MFMA (part of FOLD, separable for A/B).
-template <bool PV8, bool FOLD, bool MSUM>
+// PIPE: see the loop below (three LDS stages, next stage's Q K^T under this stage's softmax).
+template <bool PV8, bool FOLD, bool MSUM, bool PIPE = false>
 __global__ void __launch_bounds__(256, 2) attn_prefill8_kernel(
     const uint16_t* __restrict__ q, const uint8_t* __restrict__ kc, const uint8_t* __restrict__ vc,
     const int32_t* __restrict__ block_table, int bt_stride, const int32_t* __restrict__ q_start,
     const int32_t* __restrict__ ctx_len, const int32_t* __restrict__ tiles, int ntiles, uint16_t* __restrict__ out,
-    int hq, int hkv, float scale_log2, float k_scale, float v_scale) {
+    int hq, int hkv, float scale_log2, float k_scale, float v_scale, int blk_lg) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     typedef float f32x16_t __attribute__((ext_vector_type(16)));
     typedef int i32x8_t __attribute__((ext_vector_type(8)));
@@ -706,15 +707,19 @@ __global__ void __launch_bounds__(256, 2) attn_prefill8_kernel(
     const int kpg = kkey >> 4, vpg = vh * 2;
     constexpr int kStage8 = stage8_bytes<PV8>();
     uint4 ks[2], vs[2];
+    // block byte offset: a 64-bit shift when the block size is a power of two (hkv = 8: 16 KiB) instead of the
+    // int64 multiply (6 quarter-rate v_mul_lo_u32 + sign extensions per stage in the ISA)
+    // (the launcher routes only power-of-two hkv here; blk_lg = log2 of the block's bytes)
+    auto blk_off = [&](int blk) -> int64_t { return (int64_t)((uint64_t)(uint32_t)blk << blk_lg); };
     auto gload = [&](int s) {
-        const int64_t kblk = bt[min(s * 4 + kpg, nblk_m1)];
-        const uint4* kp = reinterpret_cast<const uint4*>(kc + kblk * blk_el + koffc);
+        const int kblk = bt[min(s * 4 + kpg, nblk_m1)];
+        const uint4* kp = reinterpret_cast<const uint4*>(kc + blk_off(kblk) + koffc);
         ks[0] = kp[0];
         ks[1] = kp[1];
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
-            const int64_t vblk = bt[min(s * 4 + vpg + b, nblk_m1)];
-            vs[b] = *reinterpret_cast<const uint4*>(vc + vblk * blk_el + voffc);
+            const int vblk = bt[min(s * 4 + vpg + b, nblk_m1)];
+            vs[b] = *reinterpret_cast<const uint4*>(vc + blk_off(vblk) + voffc);
         }
     };
     auto swrite = [&](int buf, int s) {
@@ -760,18 +765,22 @@ __global__ void __launch_bounds__(256, 2) attn_prefill8_kernel(
     const i32x8_t ones = {0x38383838, 0x38383838, 0x38383838, 0x38383838,
                           0x38383838, 0x38383838, 0x38383838, 0x38383838};
 
-    if (nsteps > 0) {
-        gload(0);
-        swrite(0, 0);
-    }
     const bool wave_invalid = __any(rpos < 0);
-    __syncthreads();
-    for (int s = 0; s < nsteps; ++s) {
-        if (s + 1 < nsteps) gload(s + 1);  // in flight under this stage's MFMAs
-        const unsigned char* base = lds + (s & 1) * kStage8;
-        const int t0 = s * 64;
+    // PIPE: this lane's quantised Q row in LDS after the three stages (row = w * 32 + col, 128 B, chunk c at slot
+    // c ^ ((col >> 1) & 7))
+    unsigned char* qimg = lds + 3 * kStage8 + (w * 32 + col) * 128;
+    const int qsw = (col >> 1) & 7;
+    if constexpr (PIPE) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const int u = 4 * c + 2 * hf;
+            *reinterpret_cast<i32x4_t*>(qimg + ((u ^ qsw) << 4)) = i32x4_t{qf[c][0], qf[c][1], qf[c][2], qf[c][3]};
+            *reinterpret_cast<i32x4_t*>(qimg + (((u + 1) ^ qsw) << 4)) = i32x4_t{qf[c][4], qf[c][5], qf[c][6], qf[c][7]};
+        }
+    }
+    // S^T of one stage from its LDS buffer
+    auto qk = [&](const unsigned char* base, f32x16_t (&sc)[2]) {
         // ---- S^T for the stage's two 32-key blocks: 2 fp8 MFMAs each ----
-        f32x16_t sc[2];
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
             f32x16_t acc;
@@ -789,10 +798,20 @@ __global__ void __launch_bounds__(256, 2) attn_prefill8_kernel(
                 const i32x4_t lo = *reinterpret_cast<const i32x4_t*>(base + row * 128 + ((u ^ sw) << 4));
                 const i32x4_t hi = *reinterpret_cast<const i32x4_t*>(base + row * 128 + (((u + 1) ^ sw) << 4));
                 const i32x8_t kf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-                acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(kf, qf[c], acc, 0, 0, 0, 127, 0, qe);
+                i32x8_t qv = qf[c];
+                if constexpr (PIPE) {  // Q from its LDS image (same swizzle as K): 16 VGPRs fewer across the loop
+                    const i32x4_t ql = *reinterpret_cast<const i32x4_t*>(qimg + ((u ^ qsw) << 4));
+                    const i32x4_t qh = *reinterpret_cast<const i32x4_t*>(qimg + (((u + 1) ^ qsw) << 4));
+                    qv = __builtin_shufflevector(ql, qh, 0, 1, 2, 3, 4, 5, 6, 7);
+                }
+                acc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(kf, qv, acc, 0, 0, 0, 127, 0, qe);
             }
             sc[kb] = acc;
         }
+    };
+    // mask, online softmax and P.V of stage s (S^T in sc, V in the LDS buffer at base)
+    auto smpv = [&](int s, const unsigned char* base, f32x16_t (&sc)[2]) {
+        const int t0 = s * 64;
         // ---- online softmax (v2 LEAN with the per-lane multiplier cl) ----
         const bool edge = (t0 + 64 > kv_end) || (t0 + 63 > wave_min_pos) || wave_invalid;
         if (edge) {
@@ -863,6 +882,7 @@ __global__ void __launch_bounds__(256, 2) attn_prefill8_kernel(
                 const i32x4_t hi = *reinterpret_cast<const i32x4_t*>(vr + 16);
                 const i32x8_t vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
                 o[db] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf, pf, o[db], 0, 0, 0, 127, 0, 127);
+                if constexpr (PIPE) __builtin_amdgcn_sched_barrier(0);  // one V fragment live at a time
             }
             if constexpr (kMfmaSum) lacc = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ones, pf, lacc, 0, 0, 0, 127,
                                                                                            0, 127);
@@ -889,8 +909,53 @@ __global__ void __launch_bounds__(256, 2) attn_prefill8_kernel(
             }
         }
         lsum += ps;
-        if (s + 1 < nsteps) swrite((s + 1) & 1, s + 1);
+    };
+    if constexpr (!PIPE) {
+        if (nsteps > 0) {
+            gload(0);
+            swrite(0, 0);
+        }
         __syncthreads();
+        for (int s = 0; s < nsteps; ++s) {
+            if (s + 1 < nsteps) gload(s + 1);  // in flight under this stage's MFMAs
+            const unsigned char* base = lds + (s & 1) * kStage8;
+            f32x16_t sc[2];
+            qk(base, sc);
+            smpv(s, base, sc);
+            if (s + 1 < nsteps) swrite((s + 1) & 1, s + 1);
+            __syncthreads();
+        }
+    } else {
+        // PIPE: three LDS buffers; stage s + 1's Q K^T MFMAs are issued before stage s's softmax, so the matrix pipe
+        // runs them under the exp / pack VALU (cdna_hip_programming.md T15).  Unrolled by two so the two S^T register
+        // sets swap roles without copies.
+        if (nsteps > 0) {
+            gload(0);
+            swrite(0, 0);
+        }
+        if (nsteps > 1) {
+            gload(1);
+            swrite(1, 1);
+        }
+        __syncthreads();
+        f32x16_t sa[2], sb[2];
+        if (nsteps > 0) qk(lds, sa);
+        int b0 = 0, b1 = 1, b2 = 2;  // LDS buffers of stages s, s + 1, s + 2
+        auto step = [&](int s, f32x16_t (&cur)[2], f32x16_t (&nxt)[2]) {
+            if (s + 2 < nsteps) gload(s + 2);
+            if (s + 1 < nsteps) qk(lds + b1 * kStage8, nxt);
+            smpv(s, lds + b0 * kStage8, cur);
+            if (s + 2 < nsteps) swrite(b2, s + 2);
+            __syncthreads();
+            const int t = b0;
+            b0 = b1;
+            b1 = b2;
+            b2 = t;
+        };
+        for (int s = 0; s < nsteps; s += 2) {
+            step(s, sa, sb);
+            if (s + 1 < nsteps) step(s + 1, sb, sa);
+        }
     }
 
     // ---- epilogue: lane holds O^T[dims 32 db + 8 g + 4 hf + (0..3)][its row] ----
@@ -916,11 +981,12 @@ void launch_attn_prefill(const uint16_t* q, const void* kc, const void* vc, cons
     if (ntiles == 0) return;
     // 2 (default): v2 LEAN; 5: v2 as before LEAN (kept for in-process A/B); 0 / 1: the 32-key-step kernel
     const int variant = knob("prefill_variant", 2);
-    const int f8 = fp8 && variant == 2 && block_size == 16 ? knob("prefill_fp8_mfma", 1) : 0;
+    const int f8 = fp8 && variant == 2 && block_size == 16 && (hkv & (hkv - 1)) == 0 ? knob("prefill_fp8_mfma", 1) : 0;
+    const int blk_lg = __builtin_ctz((unsigned)(hkv * 16 * kPD));
     // 1: Q K^T and P V on the fp8 MFMA; 2: Q K^T only (FOLD); 3: 1 with FOLD; 4: 2 without.  FOLD measured neutral to
     // negative with P V on the fp8 MFMA (1605 vs 1638 TFLOP/s on the 112k-prefix chunk, its 9th MFMA and the -m copies
     // cost what the removed VALU saved) and +3.8 % for Q K^T only (profiles/r5/prefill_fp8_mfma_fold_ab.jsonl)
-    if (f8 >= 1 && f8 <= 5) {  // 5: 1 with the MFMA row sums only
+    if (f8 >= 1 && f8 <= 6) {  // 5: 1 with the MFMA row sums only; 6: 1 with PIPE
         static bool attr8 = [] {
             bool ok = true;
             for (const void* f : {(const void*)attn_prefill8_kernel<true, true, true>,
@@ -928,6 +994,9 @@ void launch_attn_prefill(const uint16_t* q, const void* kc, const void* vc, cons
                                   (const void*)attn_prefill8_kernel<true, false, true>})
                 ok &= hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * stage8_bytes<true>()) ==
                       hipSuccess;
+            ok &= hipFuncSetAttribute((const void*)attn_prefill8_kernel<true, false, false, true>,
+                                      hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      3 * stage8_bytes<true>() + 16384) == hipSuccess;
             for (const void* f : {(const void*)attn_prefill8_kernel<false, true, false>,
                                   (const void*)attn_prefill8_kernel<false, false, false>})
                 ok &= hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * stage8_bytes<false>()) ==
@@ -941,11 +1010,15 @@ void launch_attn_prefill(const uint16_t* q, const void* kc, const void* vc, cons
 #define AP8_LAUNCH(PV, FO, MS)                                                                                    \
     hipLaunchKernelGGL((attn_prefill8_kernel<PV, FO, MS>), dim3(ntiles, hkv), dim3(256), 2 * stage8_bytes<PV>(), st, q, \
                        k8, v8, block_table, bt_stride, q_start, ctx_len, tiles, ntiles, out, hq, hkv, sl2, k_scale,    \
-                       v_scale)
+                       v_scale, blk_lg)
         if (f8 == 1) AP8_LAUNCH(true, false, false);
         else if (f8 == 2) AP8_LAUNCH(false, true, false);
         else if (f8 == 3) AP8_LAUNCH(true, true, true);
         else if (f8 == 5) AP8_LAUNCH(true, false, true);
+        else if (f8 == 6)
+            hipLaunchKernelGGL((attn_prefill8_kernel<true, false, false, true>), dim3(ntiles, hkv), dim3(256),
+                               3 * stage8_bytes<true>() + 16384, st, q, k8, v8, block_table, bt_stride, q_start, ctx_len, tiles,
+                               ntiles, out, hq, hkv, sl2, k_scale, v_scale, blk_lg);
         else AP8_LAUNCH(false, false, false);
 #undef AP8_LAUNCH
         return;

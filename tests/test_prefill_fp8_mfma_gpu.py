@@ -70,6 +70,8 @@ def test_fp8_mfma_prefill_vs_fp32(hq, hkv, shape):
     exp = ref.paged_attention(*args)
     truth = ref.paged_attention(*args16)  # fp32 attention on the unquantised bf16 cache
     out8 = _run(args, 1)
+    # knob 6: the same math with the next stage's Q K^T issued under the softmax (three LDS stages, Q in LDS)
+    assert torch.equal(_run(args, 6), out8)
     outqk = _run(args, 2)
     out16 = _run(args, 0)
     rel8, max8 = _errs(out8, exp)
