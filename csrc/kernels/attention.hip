@@ -1224,7 +1224,8 @@ bool launch_decode_attn_rope(const uint16_t* qkv, const int32_t* pos, const floa
                              int hq, int hkv, int block_size, float scale, hipStream_t st, const int32_t* casc,
                              uint16_t* opre, float* lpre) {
     const int nitems = n * hkv;
-    if (n == 0 || hq / hkv > 16 || block_size != 16 || nitems < 2048 || knob("decode_attn_legacy", 0) ||
+    if (n == 0 || hq / hkv > 16 || block_size != 16 || nitems < knob("decode_min_items", 1024) ||
+        knob("decode_attn_legacy", 0) ||
         knob("decode_pf", 0) || !knob("decode_lean", 1) || !knob("decode_rope_fused", 1))
         return false;
     const float scale_log2 = scale * 1.4426950408889634f;
@@ -1281,12 +1282,14 @@ void launch_paged_attn(const uint16_t* q, const void* kc, const void* vc, const 
                        float scale, bool fp8, float k_scale, float v_scale, hipStream_t st, int max_q) {
     if (ntiles == 0) return;
     const float scale_log2 = scale * 1.4426950408889634f;
-    // decode without a kv split and enough (seq, kv head) items to fill the chip one wave each (>= 2048 waves:
-    // 8 per CU); fewer items keep the split-over-waves form (profiles/r1_attn_decode.json: B=64 x 1k ctx is 1.5x
-    // faster there, B >= 256 at 128-512 ctx 1.0-1.3x slower)
+    // decode without a kv split and enough (seq, kv head) items to fill the chip one wave each; fewer items keep the
+    // split-over-waves form (profiles/r1_attn_decode.json: B=64 x 1k ctx is 1.5x faster there, B >= 256 at 128-512
+    // ctx 1.0-1.3x slower).  Threshold 2048 -> 1024 items in r5: the T = 128 bucket at 200-token contexts runs
+    // 21.7 vs 26.7 us per layer on the one-wave kernel, 6.14 -> 5.98 ms per forward; T = 64 (512 items) is neutral
+    // (profiles/r5/decode_min_items_ab.jsonl)
     const int nitems = ntiles * hkv;
     if (tiles == nullptr && nqt == 1 && nsplit == 1 && max_q == 1 && hq / hkv <= 16 && block_size == 16 &&
-        nitems >= 2048) {
+        nitems >= knob("decode_min_items", 1024)) {
         if (knob("decode_attn_legacy", 0)) goto legacy;  // A/B against the split-over-waves kernel
         const int pf = knob("decode_pf", 0);
         const bool lean = knob("decode_lean", 1) != 0;

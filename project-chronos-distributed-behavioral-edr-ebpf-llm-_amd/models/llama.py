@@ -33,7 +33,7 @@ _FUSE_AR_NORM = os.environ.get("CHRONOS_FUSE_AR_NORM", "1") != "0"
 # residual epilogues instead of W8A8 (an activation-quantisation launch per projection).  Not at T = 3-4: the GEMV's
 # per-row-group overhead makes it slower there than the W8A8 GEMMs (gate_up 140 vs 27 us, profiles/r5/w8a16_*)
 _W8A16_DECODE = os.environ.get("CHRONOS_W8A16_DECODE", "1") != "0"  # TP: fused IPC all-reduce + residual + RMSNorm
-# batched decode (>= 2048 (row, kv head) items, bf16 KV): RoPE + paged-KV write fused into the decode attention
+# batched decode (>= 1024 (row, kv head) items, bf16 KV): RoPE + paged-KV write fused into the decode attention
 _FUSE_DECODE_ROPE = os.environ.get("CHRONOS_FUSE_DECODE_ROPE", "1") != "0"
 
 

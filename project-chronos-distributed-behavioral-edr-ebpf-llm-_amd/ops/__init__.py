@@ -237,7 +237,7 @@ def decode_attention_rope(qkv, pos, cos_sin, k_cache, v_cache, block_table, ctx_
                           scale: float, casc=None):
     """Decode step (row i = sequence i, one token at pos[i], ctx_len[i] == pos[i] + 1): RoPE + paged-KV write + paged
     attention in one launch (csrc/kernels/attention.hip paged_decode_kernel RP).  Returns the [n, hq, 128] output, or
-    None when the fused kernel does not serve the shape (fp8 KV, < 2048 (row, kv head) items, ...): the caller then
+    None when the fused kernel does not serve the shape (fp8 KV, < 1024 (row, kv head) items, ...): the caller then
     runs rope_kv_write + paged_attention, which compute the same thing.
 
     ``casc``: optional (casc [1 + P_max] int32, o scratch [S, hq, 128] bf16, lse scratch [S, hq] f32) — cascade

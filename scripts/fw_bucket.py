@@ -21,11 +21,15 @@ def main():
     ap.add_argument("--ctx", type=int, default=200)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--weights", default="bf16", choices=["bf16", "fp8"])
+    ap.add_argument("--knob", action="append", default=[], help="kernel knob name=value (torch.ops.chronos.set_knob)")
     a = ap.parse_args()
     from chronos import ops
     from chronos.models.llama import KVCache, StepBatch, build_model
 
     ops.load()
+    for kv_ in a.knob:
+        name, val = kv_.split("=")
+        torch.ops.chronos.set_knob(name, int(val))
     dev = torch.device("cuda")
     m = build_model(a.model, dev, weight_dtype=a.weights)
     n, bs = a.rows, 16
@@ -57,7 +61,8 @@ def main():
     torch.cuda.synchronize()
     ms = s.elapsed_time(e) / a.iters
     wbytes = m.w.nbytes()
-    print(json.dumps({"model": a.model, "weights": a.weights, "rows": n, "ctx": a.ctx, "ms_per_forward": round(ms, 3),
+    print(json.dumps({"model": a.model, "weights": a.weights, "rows": n, "ctx": a.ctx, "knobs": a.knob,
+                      "ms_per_forward": round(ms, 3),
                       "weight_GB": round(wbytes / 1e9, 2), "weight_stream_TBps": round(wbytes / ms / 1e9, 2)}))
 
 

@@ -160,7 +160,7 @@ def test_paged_attention_decode(hq, hkv, nsplit):
 
 @pytest.mark.parametrize("hq,hkv", [(32, 8), (64, 8)])
 def test_paged_attention_decode_one_wave_kernel(hq, hkv):
-    """>= 2048 (seq, kv head) items select the one-wave-per-item decode kernel: ragged contexts from 1 token to past
+    """>= 1024 (seq, kv head) items select the one-wave-per-item decode kernel: ragged contexts from 1 token to past
     the 64-entry block-table window (1100 tokens = 69 blocks), prefetch on and off, against the fp32 reference."""
     from chronos import ops
     from chronos.ops import reference as ref
@@ -205,7 +205,7 @@ def test_decode_attention_rope_fused_matches_unfused(hq, hkv):
     exp = ops.paged_attention(qb, k2, v2, bt, qs, ctx, None, B, 1, 1)
     want = ref.paged_attention(qb, k2, v2, bt, qs, ctx, None, B, 1, 1)
     out = ops.decode_attention_rope(qkv, pos, cs, k1, v1, bt, ctx, B, hq, 1.0 / math.sqrt(128))
-    assert out is not None, "the fused kernel must serve >= 2048 (row, kv head) items"
+    assert out is not None, "the fused kernel must serve >= 1024 (row, kv head) items"
     torch.cuda.synchronize()
     _close(k1, k2, 1e-2, 1e-2)  # RoPE rounding may differ by an fma contraction
     assert torch.equal(v1, v2)
