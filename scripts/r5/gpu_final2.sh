@@ -1,0 +1,15 @@
+#!/bin/bash
+# r5 closing run 2: GPU suite (-x, as the driver), smoke, default bench, and the 128k fp8-KV + bf16-weights TTFT
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+O=gpurun_out/r5final2
+mkdir -p $O
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 150 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+timeout -k 10 600 python -u bench.py > $O/bench.log 2>&1 || { tail -30 $O/bench.log; exit 1; }
+grep '^{' $O/bench.log | tail -1 > $O/bench.json
+cut -c1-300 $O/bench.json
+timeout -k 10 300 python -u scripts/long_context.py --tokens 131000 --kv-dtype fp8 --weights bf16 --repeat 2 > $O/long_fp8kv_bf16w.log 2>&1 || { tail -20 $O/long_fp8kv_bf16w.log; exit 1; }
+grep '"run": 1' $O/long_fp8kv_bf16w.log
