@@ -775,7 +775,8 @@ __global__ void __launch_bounds__(256, 2) attn_prefill8_kernel(
         for (int c = 0; c < 2; ++c) {
             const int u = 4 * c + 2 * hf;
             *reinterpret_cast<i32x4_t*>(qimg + ((u ^ qsw) << 4)) = i32x4_t{qf[c][0], qf[c][1], qf[c][2], qf[c][3]};
-            *reinterpret_cast<i32x4_t*>(qimg + (((u + 1) ^ qsw) << 4)) = i32x4_t{qf[c][4], qf[c][5], qf[c][6], qf[c][7]};
+            *reinterpret_cast<i32x4_t*>(qimg + (((u + 1) ^ qsw) << 4)) =
+                i32x4_t{qf[c][4], qf[c][5], qf[c][6], qf[c][7]};
         }
     }
     // S^T of one stage from its LDS buffer
@@ -1007,18 +1008,18 @@ void launch_attn_prefill(const uint16_t* q, const void* kc, const void* vc, cons
         const float sl2 = scale * 1.4426950408889634f;
         const uint8_t* k8 = static_cast<const uint8_t*>(kc);
         const uint8_t* v8 = static_cast<const uint8_t*>(vc);
-#define AP8_LAUNCH(PV, FO, MS)                                                                                    \
-    hipLaunchKernelGGL((attn_prefill8_kernel<PV, FO, MS>), dim3(ntiles, hkv), dim3(256), 2 * stage8_bytes<PV>(), st, q, \
-                       k8, v8, block_table, bt_stride, q_start, ctx_len, tiles, ntiles, out, hq, hkv, sl2, k_scale,    \
-                       v_scale, blk_lg)
+#define AP8_LAUNCH(PV, FO, MS)                                                                              \
+    hipLaunchKernelGGL((attn_prefill8_kernel<PV, FO, MS>), dim3(ntiles, hkv), dim3(256), 2 * stage8_bytes<PV>(), \
+                       st, q, k8, v8, block_table, bt_stride, q_start, ctx_len, tiles, ntiles, out, hq, hkv, sl2,  \
+                       k_scale, v_scale, blk_lg)
         if (f8 == 1) AP8_LAUNCH(true, false, false);
         else if (f8 == 2) AP8_LAUNCH(false, true, false);
         else if (f8 == 3) AP8_LAUNCH(true, true, true);
         else if (f8 == 5) AP8_LAUNCH(true, false, true);
         else if (f8 == 6)
             hipLaunchKernelGGL((attn_prefill8_kernel<true, false, false, true>), dim3(ntiles, hkv), dim3(256),
-                               3 * stage8_bytes<true>() + 16384, st, q, k8, v8, block_table, bt_stride, q_start, ctx_len, tiles,
-                               ntiles, out, hq, hkv, sl2, k_scale, v_scale, blk_lg);
+                               3 * stage8_bytes<true>() + 16384, st, q, k8, v8, block_table, bt_stride, q_start,
+                               ctx_len, tiles, ntiles, out, hq, hkv, sl2, k_scale, v_scale, blk_lg);
         else AP8_LAUNCH(false, false, false);
 #undef AP8_LAUNCH
         return;
