@@ -623,7 +623,10 @@ constexpr int stage8_bytes() { return kK8Img + (PV8 ? kV8Img : kV2Img); }
 // (profiles/r5/prefill_fp8_mfma_depth_ab.jsonl).
 // MSUM (PV8 only): the row sums from the all-ones fp8 MFMA (part of FOLD, separable for A/B).
 // PIPE: see the loop below (three LDS stages, next stage's Q K^T under this stage's softmax).
-template <bool PV8, bool FOLD, bool MSUM, bool PIPE = false>
+// WPG (PV8): wave w stages page w of the stage for both K (its 16 keys) and V (all 128 dims, 2 per lane), so the
+// block id is wave-uniform — one scalar load per stage instead of three per-lane loads + 64-bit address VALU — and
+// the V^T image takes 8-byte halves (ds_write2) with no register shuffles.
+template <bool PV8, bool FOLD, bool MSUM, bool PIPE = false, bool WPG = false>
 __global__ void __launch_bounds__(256, 2) attn_prefill8_kernel(
     const uint16_t* __restrict__ q, const uint8_t* __restrict__ kc, const uint8_t* __restrict__ vc,
     const int32_t* __restrict__ block_table, int bt_stride, const int32_t* __restrict__ q_start,
@@ -711,7 +714,19 @@ __global__ void __launch_bounds__(256, 2) attn_prefill8_kernel(
     // int64 multiply (6 quarter-rate v_mul_lo_u32 + sign extensions per stage in the ISA)
     // (the launcher routes only power-of-two hkv here; blk_lg = log2 of the block's bytes)
     auto blk_off = [&](int blk) -> int64_t { return (int64_t)((uint64_t)(uint32_t)blk << blk_lg); };
+    const int wv = __builtin_amdgcn_readfirstlane(w);
+    static_assert(!WPG || PV8, "page-per-wave staging: fp8 V image");
     auto gload = [&](int s) {
+        if constexpr (WPG) {
+            const int64_t boff = blk_off(bt[min(s * 4 + wv, nblk_m1)]);  // wave-uniform
+            const uint4* kp = reinterpret_cast<const uint4*>(kc + boff + koffc);
+            ks[0] = kp[0];
+            ks[1] = kp[1];
+            const uint4* vp = reinterpret_cast<const uint4*>(vc + boff + (h * kPD + 2 * lane) * 16);
+            vs[0] = vp[0];
+            vs[1] = vp[1];
+            return;
+        }
         const int kblk = bt[min(s * 4 + kpg, nblk_m1)];
         const uint4* kp = reinterpret_cast<const uint4*>(kc + blk_off(kblk) + koffc);
         ks[0] = kp[0];
@@ -725,15 +740,28 @@ __global__ void __launch_bounds__(256, 2) attn_prefill8_kernel(
     auto swrite = [&](int buf, int s) {
         if (s * 64 + 64 > kv_end) {  // the stage reaching past kv_end: zero keys / pages past it (wave-uniform)
             if (s * 64 + kkey >= kv_end) ks[0] = ks[1] = uint4{0u, 0u, 0u, 0u};
+            if constexpr (WPG) {
+                if (s * 64 + wv * 16 >= kv_end) vs[0] = vs[1] = uint4{0u, 0u, 0u, 0u};
+            } else {
 #pragma unroll
-            for (int b = 0; b < 2; ++b)
-                if (s * 64 + vh * 32 + b * 16 >= kv_end) vs[b] = uint4{0u, 0u, 0u, 0u};
+                for (int b = 0; b < 2; ++b)
+                    if (s * 64 + vh * 32 + b * 16 >= kv_end) vs[b] = uint4{0u, 0u, 0u, 0u};
+            }
         }
         unsigned char* base = lds + buf * kStage8;
         const int sw = (kkey >> 1) & 7;
         *reinterpret_cast<uint4*>(base + kkey * 128 + (((2 * kq) ^ sw) << 4)) = ks[0];
         *reinterpret_cast<uint4*>(base + kkey * 128 + (((2 * kq + 1) ^ sw) << 4)) = ks[1];
-        if constexpr (PV8) {
+        if constexpr (WPG) {
+            // page wv = keys 32 kb + 16 b + 4 wd + 0..3 (kb = wv >> 1, b = wv & 1): word wd -> half wd & 1, dword
+            // 2b + (wd >> 1) of 16-B block kb, i.e. {x, z} -> half 0, {y, w} -> half 1, 8 bytes each
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                unsigned char* vr = base + kK8Img + (2 * lane + j) * kV8Pitch + (wv >> 1) * 16 + (wv & 1) * 8;
+                *reinterpret_cast<uint2*>(vr) = uint2{vs[j].x, vs[j].z};
+                *reinterpret_cast<uint2*>(vr + 32) = uint2{vs[j].y, vs[j].w};
+            }
+        } else if constexpr (PV8) {
             // page b word wd = keys vh*32 + 16b + 4wd + 0..3 -> half wd & 1, dword 2b + (wd >> 1) of 16-B block vh
             unsigned char* vr = base + kK8Img + vdim * kV8Pitch + vh * 16;
             *reinterpret_cast<uint4*>(vr) = uint4{vs[0].x, vs[0].z, vs[1].x, vs[1].z};
@@ -987,11 +1015,13 @@ void launch_attn_prefill(const uint16_t* q, const void* kc, const void* vc, cons
     // 1: Q K^T and P V on the fp8 MFMA; 2: Q K^T only (FOLD); 3: 1 with FOLD; 4: 2 without.  FOLD measured neutral to
     // negative with P V on the fp8 MFMA (1605 vs 1638 TFLOP/s on the 112k-prefix chunk, its 9th MFMA and the -m copies
     // cost what the removed VALU saved) and +3.8 % for Q K^T only (profiles/r5/prefill_fp8_mfma_fold_ab.jsonl)
-    if (f8 >= 1 && f8 <= 6) {  // 5: 1 with the MFMA row sums only; 6: 1 with PIPE
+    // 5: 1 with the MFMA row sums only; 6: 1 with PIPE; 7: 1 with per-lane block ids (before WPG)
+    if (f8 >= 1 && f8 <= 7) {
         static bool attr8 = [] {
             bool ok = true;
             for (const void* f : {(const void*)attn_prefill8_kernel<true, true, true>,
                                   (const void*)attn_prefill8_kernel<true, false, false>,
+                                  (const void*)attn_prefill8_kernel<true, false, false, false, true>,
                                   (const void*)attn_prefill8_kernel<true, false, true>})
                 ok &= hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * stage8_bytes<true>()) ==
                       hipSuccess;
@@ -1012,7 +1042,11 @@ void launch_attn_prefill(const uint16_t* q, const void* kc, const void* vc, cons
     hipLaunchKernelGGL((attn_prefill8_kernel<PV, FO, MS>), dim3(ntiles, hkv), dim3(256), 2 * stage8_bytes<PV>(), \
                        st, q, k8, v8, block_table, bt_stride, q_start, ctx_len, tiles, ntiles, out, hq, hkv, sl2,  \
                        k_scale, v_scale, blk_lg)
-        if (f8 == 1) AP8_LAUNCH(true, false, false);
+        if (f8 == 1)
+            hipLaunchKernelGGL((attn_prefill8_kernel<true, false, false, false, true>), dim3(ntiles, hkv), dim3(256),
+                               2 * stage8_bytes<true>(), st, q, k8, v8, block_table, bt_stride, q_start, ctx_len, tiles,
+                               ntiles, out, hq, hkv, sl2, k_scale, v_scale, blk_lg);
+        else if (f8 == 7) AP8_LAUNCH(true, false, false);
         else if (f8 == 2) AP8_LAUNCH(false, true, false);
         else if (f8 == 3) AP8_LAUNCH(true, true, true);
         else if (f8 == 5) AP8_LAUNCH(true, false, true);
