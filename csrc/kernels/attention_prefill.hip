@@ -603,6 +603,8 @@ __global__ void __launch_bounds__(256, 2) attn_prefill2_kernel(
 // (tests/test_prefill_fp8_mfma_gpu.py checks against the fp32 reference on the dequantised cache).
 // ------------------------------------------------------------------------------------------------------------------
 constexpr int kK8Img = 64 * 128;
+// key <-> K image row within a 16-key page: bits 2 and 3 swapped (an involution)
+__device__ __forceinline__ int kperm(int k) { return (k & ~12) | ((k >> 1) & 4) | ((k << 1) & 8); }
 constexpr int kV8Pitch = 80;
 constexpr int kV8Img = 128 * kV8Pitch;
 template <bool PV8>
@@ -749,17 +751,19 @@ __global__ void __launch_bounds__(256, 2) attn_prefill8_kernel(
             }
         }
         unsigned char* base = lds + buf * kStage8;
-        const int sw = (kkey >> 1) & 7;
-        *reinterpret_cast<uint4*>(base + kkey * 128 + (((2 * kq) ^ sw) << 4)) = ks[0];
-        *reinterpret_cast<uint4*>(base + kkey * 128 + (((2 * kq + 1) ^ sw) << 4)) = ks[1];
+        const int krow = WPG ? kperm(kkey) : kkey;
+        const int sw = (krow >> 1) & 7;
+        *reinterpret_cast<uint4*>(base + krow * 128 + (((2 * kq) ^ sw) << 4)) = ks[0];
+        *reinterpret_cast<uint4*>(base + krow * 128 + (((2 * kq + 1) ^ sw) << 4)) = ks[1];
         if constexpr (WPG) {
-            // page wv = keys 32 kb + 16 b + 4 wd + 0..3 (kb = wv >> 1, b = wv & 1): word wd -> half wd & 1, dword
-            // 2b + (wd >> 1) of 16-B block kb, i.e. {x, z} -> half 0, {y, w} -> half 1, 8 bytes each
+            // K rows are stored with key bits 2 and 3 swapped (kperm), so S^T lane half hf holds keys with bit 3 = hf:
+            // page wv = keys 32 kb + 16 b + t (kb = wv >> 1, b = wv & 1) -> half t >> 3, bytes 16 kb + 8 b + (t & 7),
+            // i.e. words {x, y} -> half 0 and {z, w} -> half 1, 8 contiguous bytes each (no register shuffles)
 #pragma unroll
             for (int j = 0; j < 2; ++j) {
                 unsigned char* vr = base + kK8Img + (2 * lane + j) * kV8Pitch + (wv >> 1) * 16 + (wv & 1) * 8;
-                *reinterpret_cast<uint2*>(vr) = uint2{vs[j].x, vs[j].z};
-                *reinterpret_cast<uint2*>(vr + 32) = uint2{vs[j].y, vs[j].w};
+                *reinterpret_cast<uint2*>(vr) = uint2{vs[j].x, vs[j].y};
+                *reinterpret_cast<uint2*>(vr + 32) = uint2{vs[j].z, vs[j].w};
             }
         } else if constexpr (PV8) {
             // page b word wd = keys vh*32 + 16b + 4wd + 0..3 -> half wd & 1, dword 2b + (wd >> 1) of 16-B block vh
@@ -844,12 +848,17 @@ __global__ void __launch_bounds__(256, 2) attn_prefill8_kernel(
         // ---- online softmax (v2 LEAN with the per-lane multiplier cl) ----
         const bool edge = (t0 + 64 > kv_end) || (t0 + 63 > wave_min_pos) || wave_invalid;
         if (edge) {
-            const int lim = min(kv_end, rpos + 1) - (t0 + 4 * hf);
+            // S^T register i of block kb, lane half hf = K image row kb*32 + (i&3) + 8(i>>2) + 4hf; WPG stores key
+            // kperm(row) there (bits 2 and 3 swapped)
+            const int lim = min(kv_end, rpos + 1) - (t0 + (WPG ? 8 : 4) * hf);
 #pragma unroll
             for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-                for (int i = 0; i < 16; ++i)
-                    sc[kb][i] = (kb * 32 + (i & 3) + 8 * (i >> 2)) >= lim ? -INFINITY : sc[kb][i];
+                for (int i = 0; i < 16; ++i) {
+                    const int ko = WPG ? kb * 32 + (i & 3) + 4 * ((i >> 2) & 1) + 16 * (i >> 3)
+                                       : kb * 32 + (i & 3) + 8 * (i >> 2);
+                    sc[kb][i] = ko >= lim ? -INFINITY : sc[kb][i];
+                }
         }
         float mx = -INFINITY;
 #pragma unroll
