@@ -269,7 +269,11 @@ constexpr int kV2Img = 128 * kV2Pitch;  // V^T image bytes per stage
 constexpr int kStage2 = kK2Img + kV2Img;
 constexpr float kRescaleThr = 8.f;     // defer-max threshold (log2 units)
 
-template <bool FP8, bool LEAN>
+// WPG (bf16 LEAN, default; knob prefill_wpg=0 for the per-lane form): wave w stages page w of the stage for K and V
+// (2 dims of V per lane), so the block id is wave-uniform — a scalar load per stage instead of three per-lane loads
+// (attn_prefill8_kernel's WPG, +6.8 % there).  bf16, bit-identical: +0.4-1.6 % on 16k chunks (MFMA-heavier than fp8),
+// +8.6 % on the 1024-stream wave's 93-token prompts (profiles/r5/prefill_bf16_wpg_ab.jsonl).
+template <bool FP8, bool LEAN, bool WPG = false>
 __global__ void __launch_bounds__(256, 2) attn_prefill2_kernel(
     const uint16_t* __restrict__ q, const void* __restrict__ kcv, const void* __restrict__ vcv,
     const int32_t* __restrict__ block_table, int bt_stride, const int32_t* __restrict__ q_start,
@@ -331,7 +335,22 @@ __global__ void __launch_bounds__(256, 2) attn_prefill2_kernel(
     const int koffc = (h * 16 + (kkey & 15)) * kPD + kq * 32;      // K: this thread's 64 B of its key
     const int voffc = (h * kPD + vdim) * 16;                       // V^T: this thread's dim row of a page
     const int kpg = kkey >> 4, vpg = vh * 2;
+    static_assert(!WPG || (LEAN && !FP8), "page-per-wave staging: bf16 LEAN");
+    const int wv = __builtin_amdgcn_readfirstlane(w);
     auto gload_lean = [&](int s) {
+        if constexpr (WPG) {
+            const int64_t blk = bt[min(s * 4 + wv, nblk_m1)];  // wave-uniform
+            const u16x8* kp = reinterpret_cast<const u16x8*>(kc + blk * blk_el + koffc);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) ks[j] = kp[j];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const u16x8* vp = reinterpret_cast<const u16x8*>(vc + blk * blk_el + (h * kPD + 2 * lane + j) * 16);
+                vs[2 * j] = vp[0];
+                vs[2 * j + 1] = vp[1];
+            }
+            return;
+        }
         const int64_t kblk = bt[min(s * 4 + kpg, nblk_m1)];
         if constexpr (FP8) {
             const uint4* p = reinterpret_cast<const uint4*>(reinterpret_cast<const uint8_t*>(kcv) + kblk * blk_el + koffc);
@@ -421,11 +440,17 @@ __global__ void __launch_bounds__(256, 2) attn_prefill2_kernel(
                 const uint16_t km = s * 64 + kkey < kv_end ? 0xFFFF : 0;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) ks[j] &= km;
+                if constexpr (WPG) {
+                    const uint16_t vm = s * 64 + wv * 16 < kv_end ? 0xFFFF : 0;
 #pragma unroll
-                for (int b = 0; b < 2; ++b) {
-                    const uint16_t vm = s * 64 + vh * 32 + b * 16 < kv_end ? 0xFFFF : 0;
-                    vs[2 * b] &= vm;
-                    vs[2 * b + 1] &= vm;
+                    for (int j = 0; j < 4; ++j) vs[j] &= vm;
+                } else {
+#pragma unroll
+                    for (int b = 0; b < 2; ++b) {
+                        const uint16_t vm = s * 64 + vh * 32 + b * 16 < kv_end ? 0xFFFF : 0;
+                        vs[2 * b] &= vm;
+                        vs[2 * b + 1] &= vm;
+                    }
                 }
             }
         }
@@ -434,6 +459,18 @@ __global__ void __launch_bounds__(256, 2) attn_prefill2_kernel(
         for (int j = 0; j < 4; ++j) {
             const int u = (kq * 4 + j) ^ (kkey & 15);
             *reinterpret_cast<u16x8*>(base + kkey * 256 + u * 16) = ks[j];
+        }
+        if constexpr (WPG) {  // dims 2 lane + j, keys of page wv = 16-key group wv (byte offset 32 wv of the row)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                unsigned char* vp = base + kK2Img + (2 * lane + j) * kV2Pitch + wv * 32;
+                const u16x8 lo = vs[2 * j], hi = vs[2 * j + 1];
+                *reinterpret_cast<u16x4*>(vp) = u16x4{lo[0], lo[1], lo[2], lo[3]};
+                *reinterpret_cast<u16x4*>(vp + 16) = u16x4{lo[4], lo[5], lo[6], lo[7]};
+                *reinterpret_cast<u16x4*>(vp + 8) = u16x4{hi[0], hi[1], hi[2], hi[3]};
+                *reinterpret_cast<u16x4*>(vp + 24) = u16x4{hi[4], hi[5], hi[6], hi[7]};
+            }
+            return;
         }
         unsigned char* vr = base + kK2Img + vdim * kV2Pitch + vh * 64;
 #pragma unroll
@@ -1073,6 +1110,7 @@ void launch_attn_prefill(const uint16_t* q, const void* kc, const void* vc, cons
             for (const void* f : {(const void*)attn_prefill2_kernel<false, false>,
                                   (const void*)attn_prefill2_kernel<true, false>,
                                   (const void*)attn_prefill2_kernel<false, true>,
+                                  (const void*)attn_prefill2_kernel<false, true, true>,
                                   (const void*)attn_prefill2_kernel<true, true>})
                 ok &= hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kStage2) == hipSuccess;
             return ok;
@@ -1084,7 +1122,9 @@ void launch_attn_prefill(const uint16_t* q, const void* kc, const void* vc, cons
                        kc, vc, block_table, bt_stride, q_start, ctx_len, tiles, ntiles, out, hq, hkv, block_size, sl2, KS, \
                        VS)
         if (variant == 2 && block_size == 16) {
-            if (fp8) AP2_LAUNCH(true, true, k_scale, v_scale); else AP2_LAUNCH(false, true, 1.f, 1.f);
+            if (fp8) AP2_LAUNCH(true, true, k_scale, v_scale);
+            else if (knob("prefill_wpg", 1)) AP2_LAUNCH(false, true, 1.f, 1.f, true);
+            else AP2_LAUNCH(false, true, 1.f, 1.f);
         } else {
             if (fp8) AP2_LAUNCH(true, false, k_scale, v_scale); else AP2_LAUNCH(false, false, 1.f, 1.f);
         }
