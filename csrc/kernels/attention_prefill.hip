@@ -1062,12 +1062,14 @@ void launch_attn_prefill(const uint16_t* q, const void* kc, const void* vc, cons
     // negative with P V on the fp8 MFMA (1605 vs 1638 TFLOP/s on the 112k-prefix chunk, its 9th MFMA and the -m copies
     // cost what the removed VALU saved) and +3.8 % for Q K^T only (profiles/r5/prefill_fp8_mfma_fold_ab.jsonl)
     // 5: 1 with the MFMA row sums only; 6: 1 with PIPE; 7: 1 with per-lane block ids (before WPG)
-    if (f8 >= 1 && f8 <= 7) {
+    // 8: 1 with the MFMA row sums (MSUM) on top of the page-per-wave staging
+    if (f8 >= 1 && f8 <= 8) {
         static bool attr8 = [] {
             bool ok = true;
             for (const void* f : {(const void*)attn_prefill8_kernel<true, true, true>,
                                   (const void*)attn_prefill8_kernel<true, false, false>,
                                   (const void*)attn_prefill8_kernel<true, false, false, false, true>,
+                                  (const void*)attn_prefill8_kernel<true, false, true, false, true>,
                                   (const void*)attn_prefill8_kernel<true, false, true>})
                 ok &= hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 2 * stage8_bytes<true>()) ==
                       hipSuccess;
@@ -1093,6 +1095,10 @@ void launch_attn_prefill(const uint16_t* q, const void* kc, const void* vc, cons
                                2 * stage8_bytes<true>(), st, q, k8, v8, block_table, bt_stride, q_start, ctx_len, tiles,
                                ntiles, out, hq, hkv, sl2, k_scale, v_scale, blk_lg);
         else if (f8 == 7) AP8_LAUNCH(true, false, false);
+        else if (f8 == 8)
+            hipLaunchKernelGGL((attn_prefill8_kernel<true, false, true, false, true>), dim3(ntiles, hkv), dim3(256),
+                               2 * stage8_bytes<true>(), st, q, k8, v8, block_table, bt_stride, q_start, ctx_len, tiles,
+                               ntiles, out, hq, hkv, sl2, k_scale, v_scale, blk_lg);
         else if (f8 == 2) AP8_LAUNCH(false, true, false);
         else if (f8 == 3) AP8_LAUNCH(true, true, true);
         else if (f8 == 5) AP8_LAUNCH(true, false, true);
