@@ -81,6 +81,11 @@ def test_fp8_mfma_prefill_vs_fp32(hq, hkv, shape):
     rel8, max8 = _errs(out8, exp)
     relqk, maxqk = _errs(outqk, exp)
     rel16, max16 = _errs(out16, exp)
+    # the A/B variants reachable through the knob (3: folded scale + MFMA row sums, 4: Q K^T only unfolded, 5 / 8:
+    # MFMA row sums on the per-lane / page-per-wave staging) compute the same attention
+    for var in (3, 4, 5, 8):
+        relv, _ = _errs(_run(args, var), exp)
+        assert relv < (0.035 if var == 4 else 0.05), (var, relv)
     print(f"fp8-MFMA rel {rel8:.4f} max {max8:.4f} | QK-only rel {relqk:.4f} max {maxqk:.4f} | "
           f"bf16-MFMA rel {rel16:.4f} max {max16:.4f}")
     # against the bf16-cache truth: what the e4m3 cache alone costs vs what the fp8 MFMA adds on top
