@@ -36,10 +36,11 @@ constexpr int kLGConfigs = 28;
 // gemm_lg 72-75 (32-row x tiles, after the 40-71 timing-ablation ids), 76-77 (192 W x 128 x rows: 256 tiles at
 // N = 6144, M = 1024 — one round on 256 CUs) and 78-79 (32-row x tiles with 7 / 12-stage rings: mid-M weight streams
 // are bound by the W bytes in flight per CU, so nearly all of the 160 KiB LDS holds W stages) and 80 (cfg 20's slab
-// schedule on 32x32x16 MFMAs)
-constexpr int kLGTinyFirst = 72, kLGTinyConfigs = 9;
+// schedule on 32x32x16 MFMAs) and 81-90 (4 waves, 128 x 128 per wave, the three-barrier slab loop: VAR 4-60 in gemm_lg.hip)
+constexpr int kLGTinyFirst = 72, kLGTinyConfigs = 19;
 int gemm_lg_xm(int cfg);  // x rows per tile
 int gemm_lg_wn(int cfg);  // W rows per tile
+bool gemm_lg_splitk_ok(int cfg);  // false for the HB configs (VAR 4): no split-K path
 bool gemm_lg_ablations_built();  // the timing-only ablation ids 40-71 exist (CHRONOS_GEMM_ABLATIONS build)
 bool launch_gemm_lg(int cfg, int mode, bool normp, const PPArgs& a, hipStream_t st);
 // W8A8 fp8 configs of the same kernel (ring schedule, 128-deep stages; a.kts counts 128-deep units), own id space

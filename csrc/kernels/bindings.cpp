@@ -560,6 +560,7 @@ std::tuple<Tensor, Tensor> gemm_pp(const Tensor& x, const Tensor& w, int64_t mod
     CHK(!lg || ((N + BN) * K * 2 < (1LL << 31) && (M + BM) * K * 2 < (1LL << 31)), "gemm_lg: operand > 2 GiB");
     CHK(M >= 1 && M < (1LL << 31) / BM && K % 64 == 0 && K <= (1 << 20) && N * K < (1LL << 40), "gemm_pp: size");
     CHK(splitk >= 1 && (K / 64) % splitk == 0, "gemm_pp: splitk must divide K / 64");
+    CHK(!lg || splitk == 1 || chronos::gemm_lg_splitk_ok((int)cfg), "gemm_lg: this config has no split-K");
     CHK(mode == 0 ? N % 4 == 0 : N % BN == 0, "gemm_pp: N % 4 (plain) / N % BN (swiglu, resid)");
     CHK(mode != 1 || (lg ? (BN / 4) % 16 == 0 : (BN / 8) % 16 == 0), "gemm_pp: swiglu needs BN >= 128 (gemm_lg: 64)");
     CHK(mode != 2 || !part_in.has_value(), "gemm_pp: resid mode has no norm prologue");

@@ -32,6 +32,7 @@
 #include "chronos_gemm.h"
 
 #include <type_traits>
+#include <utility>
 
 namespace chronos {
 namespace {
@@ -86,11 +87,35 @@ __device__ __forceinline__ void lg_dma16(const void* base, int bytes, unsigned c
 // The same piece as inline asm (VAR 2): M0 = the LDS destination, written in the same statement that reads it
 // (cdna_hip_programming.md §5.7).  No VGPR destination; completion is counted by the kernel's own vmcnt waits.
 typedef int lg_i32x4 __attribute__((ext_vector_type(4)));
+template <bool NOP = true>
 __device__ __forceinline__ void lg_dma16_asm(const void* base, int bytes, uint32_t lds, uint32_t voff, int soff) {
     const uint64_t b = (uint64_t)base;
     const lg_i32x4 r = {(int)(uint32_t)b, (int)(uint32_t)(b >> 32), bytes, 0x00020000};
-    asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds"
-                 ::"v"(voff), "s"(r), "s"(lds), "s"(soff) : "memory");
+    if constexpr (NOP)
+        asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds"
+                     ::"v"(voff), "s"(r), "s"(lds), "s"(soff) : "memory");
+    else  // (hipBLASLt's gfx950 code issues the LDS-DMA right after its M0 write)
+        asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, %3 offen lds"
+                     ::"v"(voff), "s"(r), "s"(lds), "s"(soff) : "memory");
+}
+
+// HB: image row of W fragment block s relative to block 0 (SwiGLU: gate blocks 0 .. 3, then the up blocks at WN / 2)
+constexpr int hb_wrow(int s, bool swiglu, int WN) { return swiglu ? (s < 4 ? 16 * s : WN / 2 + 16 * (s - 4)) : 16 * s; }
+
+// HB slab schedule: the DMA piece issued before MFMA i of the 128 (-1: none).  Pieces 0 .. NPW-1 are W, the rest x.
+constexpr int hb_piece(int i, int B1, int B2, int B3, int DX, int DW, int NPW, int NPX) {
+    return (i >= B1 && i < B2 && (i - B1) % DX == 0 && (i - B1) / DX < NPX) ? NPW + (i - B1) / DX
+           : (i >= B2 && i < B3 && (i - B2) % DW == 0 && (i - B2) / DW < NPW) ? (i - B2) / DW
+                                                                              : -1;
+}
+// hipBLASLt's distribution: x pieces 0-4 after B1 and 5-7 after B2 (every 2 MFMAs), W pieces 0-4 spread over
+// B2+8 .. B3 and 5-7 after B3
+constexpr int hb_piece_lib(int i, int B1, int B2, int B3, int NPW, int NPX) {
+    return (i >= B1 && i < B1 + 10 && (i - B1) % 2 == 0) ? NPW + (i - B1) / 2
+           : (i >= B2 && i < B2 + 6 && (i - B2) % 2 == 0) ? NPW + 5 + (i - B2) / 2
+           : (i >= B2 + 8 && i < B2 + 58 && (i - B2 - 8) % 10 == 0) ? (i - B2 - 8) / 10
+           : (i >= B3 + 4 && i < B3 + 16 && (i - B3 - 4) % 4 == 0) ? 5 + (i - B3 - 4) / 4
+                                                                    : -1;
 }
 
 // W8A8 fp8 (F8): a fragment of v_mfma_scale_f32_16x16x128_f8f6f4 is 32 k-bytes per lane (two 16-B chunks)
@@ -101,6 +126,12 @@ __device__ __forceinline__ f32x4 lg_mma(const bf16x8& a, const bf16x8& b, f32x4 
 // block-scaled form fed the unit MX exponent (127 = 2^0): the per-token / per-channel scales go in the epilogue
 __device__ __forceinline__ f32x4 lg_mma(const lg_i32x8& a, const lg_i32x8& b, f32x4 c) {
     return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
+}
+
+// f(std::integral_constant<int, I>{}) for every I of the sequence, in order (a compile-time unrolled loop)
+template <typename F, int... Is>
+__device__ __forceinline__ void lg_static_for(F&& f, std::integer_sequence<int, Is...>) {
+    (f(std::integral_constant<int, Is>{}), ...);
 }
 
 // 64-B-row chunk swizzle (the 16x16x32 fragment reads of a 16-row block land on 16 distinct 16-B slots)
@@ -125,6 +156,18 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
     // halves); the accumulators are copied into the 16x16 register order before split-K / the epilogue, which then
     // maps (block, register) -> (n, m) with the 32x32 output layout
     constexpr bool M32 = VAR == 3;
+    // VAR 4 (HB): one wave per SIMD (NWX = 2), 128 x 128 outputs per wave, and the slab loop of three barriers per
+    // 64-deep slab (profiles/r6_gemm_isa_diff.md): the wave reads ALL of slab j's fragments into registers early (k-step
+    // 0 at the end of slab j-1, k-step 1 in the first quarter of slab j), so the slab's LDS buffer is released per
+    // operand after a quarter (x) / half (W) of the slab and slab j+2's LDS-DMA gets ~1.5 slabs to land (vmcnt counted,
+    // never 0); every wave stages a share of both operands, so each release barrier is followed by DMA on all waves
+    // HB variants (timing study, VAR 5-11 = 4 + bits; every one computes the same result): bit 0 LDS-DMA pieces
+    // without the s_nop after the M0 write; bit 1 hipBLASLt's DMA distribution (x: 5 pieces after B1 + 3 after B2,
+    // W: 5 after B2 + 3 after B3, vmcnt(13)); bit 2 lgkmcnt(0) before the slab's last MFMA instead of hipcc's counted
+    // waits at the next slab's head; bit 3 precomputed addressing (below); bit 4 LDS-staged epilogue; bit 5 the next
+    // slab's reads from MFMA 94 (below)
+    constexpr bool HB = VAR >= 4 && VAR < 68;
+    constexpr int HBV = HB ? VAR - 4 : 0;
     constexpr int ES = F8 ? 1 : 2;  // operand bytes per element
     static_assert(!F8 || (ST >= 3 && RB == 128 && MODE != kResid && !NORMP && VAR == 0 && ABL == 0),
                   "fp8: ring schedule, 128-B rows, plain / SwiGLU epilogue");
@@ -147,6 +190,7 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
     static_assert(!STG || (SLAB && NWX == 4), "staggered DMA: slab schedule, two waves per SIMD");
     static_assert(!MAN || SLAB, "issue-ordered k-steps: slab schedule");
     static_assert(!M32 || (SLAB && !F8 && ABL == 0 && NT % 2 == 0 && MT % 2 == 0), "32x32 MFMA: slab schedule, bf16");
+    static_assert(!HB || (SLAB && !F8 && ABL == 0 && NWX == 2 && NT == 8 && MT == 8), "HB: 256 x 256 slab, 4 waves");
     static_assert(ST >= 3 || (SLAB && RB == 128), "slab schedule: 64-deep (128-B row) slabs");
     static_assert(MODE != kSwiglu || (WN / 4) % 16 == 0, "swiglu: WN/4 gate rows per wave, multiple of 16");
     static_assert(RB == 64 || RB == 128, "stage depth 32 or 64");
@@ -186,9 +230,11 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
     uint32_t voff[NPER];
     int dsto[NPER];
     bool isw[NPER];
+    // HB: wave w stages W image pieces [w NPW, +NPW) (pieces 0 .. NPW-1 of its list) and x pieces [w NPX, +NPX)
+    constexpr int NPW = WN / RPI / NW, NPX = XM / RPI / NW;
 #pragma unroll
     for (int i = 0; i < NPER; ++i) {
-        const int q = wave * NPER + i;
+        const int q = HB ? (i < NPW ? wave * NPW + i : WN / RPI + wave * NPX + (i - NPW)) : wave * NPER + i;
         const int r = q * RPI + lane / (RB / 16);
         const int pc = lane % (RB / 16);
         dsto[i] = q * 1024;
@@ -365,7 +411,18 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
             lg_vmcnt<NPER>();  // slab 0 landed (slab 1 in flight)
         }
         lg_bar();
-        rd(0, 0, fa0, fb0);
+        if constexpr (HB) {
+            // the order of the loop's set-0 reads (fa[0], fb[*], fa[1..]): the same pending-read state enters the loop
+            // from the prologue and from the back edge, so hipcc's waits at the first MFMAs stay counted
+            fa0[0] = *reinterpret_cast<const bf16x8*>(smem + wrow0[0] * RB + loff[0]);
+#pragma unroll
+            for (int t = 0; t < MT; ++t)
+                fb0[t] = *reinterpret_cast<const bf16x8*>(smem + WIMG + (xrow0 + 16 * t) * RB + loff[0]);
+#pragma unroll
+            for (int s = 1; s < NT; ++s) fa0[s] = *reinterpret_cast<const bf16x8*>(smem + wrow0[s] * RB + loff[0]);
+        } else {
+            rd(0, 0, fa0, fb0);
+        }
         // STG: one straight-line loop per wave group (the DMA sits in a different k-step), so each keeps its
         // compile-time interleave
         // MAN: k-step in issue order.  MFMA i of the block is (W block i / MT, x block i % MT); DMA piece d goes before
@@ -403,6 +460,168 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
                 if (i % DS == DS - 1) __builtin_amdgcn_sched_barrier(0);
             }
         };
+        if constexpr (HB) {
+            // slab j, MFMA i of 128 (k-step i / 64; W block s = (i % 64) / 8, x block t = i % 8), issue order pinned:
+            //   i = 1, 3, .. 15 : ds_read of slab j k-step 1 x fragments (set 1)
+            //   B1 (before 22)  : lgkmcnt(0) + barrier — every wave holds slab j's x fragments: x buffer released
+            //   22 .. 51        : the wave's NPX x pieces of slab j+2 (one per 3 MFMAs) + slab j k-step 1 W reads
+            //   B2 (before 52)  : lgkmcnt(0) + barrier — W buffer released
+            //   52 .. 111       : the wave's NPW W pieces of slab j+2 (one per 7 MFMAs)
+            //   B3 (before 112) : vmcnt(NPER) (this wave's slab j+1 pieces landed; slab j+2's stay in flight) + barrier
+            //   112 .. 127      : ds_read of slab j+1 k-step 0 (set 0): fa[0], fb[0..7], fa[1..7]
+            // hipcc inserts the counted lgkmcnt waits of the set-0 reads at the next slab's first MFMAs.
+            // bit 5 (HBV & 32): hipBLASLt's B3 placement — the next slab's fragment reads start at MFMA 94 and are
+            // spread one per two MFMAs (instead of one per MFMA from 112), the W pieces one per 5 MFMAs before it
+            constexpr int MFK = NT * MT, B1 = 22, B2 = 52, B3 = (HBV & 32) ? 94 : 2 * MFK - (NT + MT);
+            constexpr int RSP = (HBV & 32) ? 2 : 1;  // MFMAs per set-0 read after B3
+            constexpr int DX = 3, DW = (HBV & 32) ? 5 : 7;
+            static_assert(NPW == 8 && NPX == 8, "HB: 8 W + 8 x pieces per wave and slab");
+            const int pstride = RPI * K * ES;  // source bytes between a wave's consecutive pieces of one operand
+            static_assert(B1 >= 2 * MT + 2 && B1 + DX * NPX <= B2 && B1 + 1 + 3 * NT <= B2 && B2 + DW * NPW <= B3 &&
+                              B3 + RSP * (NT + MT) <= 2 * MFK,
+                          "HB schedule");
+            // the accumulators live in AGPRs across the whole loop: pinned at both ends, so the epilogue's VGPR use
+            // (resid / SwiGLU / norm-scale forms) cannot make the register allocator shuffle them inside the loop
+            auto pin_acc = [&]() {
+#pragma unroll
+                for (int s = 0; s < NT; ++s)
+#pragma unroll
+                    for (int t = 0; t < MT; ++t) asm volatile("" : "+a"(acc[s][t]));
+            };
+            pin_acc();
+            if constexpr (HBV & 8) {
+                // precomputed addressing: the slab loop unrolled by two, so each half's LDS buffer is a compile-time
+                // parity; fragment reads from 8 per-lane base VGPRs (parity x operand x k-step) + immediate offsets;
+                // the LDS-DMA destination kept in M0 (one s_mov per operand and slab, then s_add 1 KiB per piece, as
+                // hipBLASLt's gfx950 code does: nothing else in the loop uses M0) and the source's k offset folded
+                // into the descriptor base once per slab, so a piece's scalar offset is a loop-invariant row stride
+                const unsigned char* rbw[2][2];
+                const unsigned char* rbx[2][2];
+#pragma unroll
+                for (int p = 0; p < 2; ++p)
+#pragma unroll
+                    for (int kk = 0; kk < 2; ++kk) {
+                        rbw[p][kk] = smem + p * STAGE + wrow0[0] * RB + loff[kk];
+                        rbx[p][kk] = smem + p * STAGE + WIMG + xrow0 * RB + loff[kk];
+                    }
+                uint32_t m0w[2], m0x[2];
+#pragma unroll
+                for (int p = 0; p < 2; ++p) {
+                    m0w[p] = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uintptr_t)(smem + p * STAGE + dsto[0]));
+                    m0x[p] = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uintptr_t)(smem + p * STAGE + dsto[NPW]));
+                }
+                const uint32_t vw = voff[0], vx = voff[NPW];
+                auto half = [&](auto PC, int j) {
+                    constexpr int P = decltype(PC)::value;  // slab j lives in buffer P, slab j+1 in 1 - P
+                    const int kb = min(j + 2, NS1) * RB;
+                    const void* bw = (const unsigned char*)a.w + kb;
+                    const void* bx = (const unsigned char*)a.x + kb;
+                    const int nw = wbytes - kb, nx = xbytes - kb;
+                    auto slot = [&](auto IC) {
+                        constexpr int i = decltype(IC)::value;
+                        if constexpr (i == B1 || i == B2) {
+                            __builtin_amdgcn_s_waitcnt(0xC07F);
+                            lg_bar();
+                        }
+                        if constexpr (i == B3) {
+                            lg_vmcnt<(HBV & 2) ? 13 : NPER>();
+                            lg_bar();
+                        }
+                        if constexpr ((HBV & 4) && i == 2 * MFK - 1) __builtin_amdgcn_s_waitcnt(0xC07F);
+                        constexpr int piece = (HBV & 2) ? hb_piece_lib(i, B1, B2, B3, NPW, NPX)
+                                                        : hb_piece(i, B1, B2, B3, DX, DW, NPW, NPX);
+                        if constexpr (piece >= 0) {
+                            constexpr bool isW = piece < NPW;
+                            constexpr int q = isW ? piece : piece - NPW;
+                            const uint64_t b = (uint64_t)(isW ? bw : bx);
+                            const lg_i32x4 r = {(int)(uint32_t)b, (int)(uint32_t)(b >> 32), isW ? nw : nx, 0x00020000};
+                            if constexpr (q == 0)
+                                asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
+                                             ::"v"(isW ? vw : vx), "s"(r), "s"(isW ? m0w[P] : m0x[P]) : "memory");
+                            else
+                                asm volatile("s_add_u32 m0, m0, 0x400\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds"
+                                             ::"v"(isW ? vw : vx), "s"(r), "s"(q * pstride) : "memory");
+                        }
+                        constexpr int ii = i % MFK, s = ii / MT, t = ii % MT;
+                        if constexpr (i < MFK)
+                            acc[s][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0[s], fb0[t], acc[s][t], 0, 0, 0);
+                        else
+                            acc[s][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1[s], fb1[t], acc[s][t], 0, 0, 0);
+                        if constexpr (i < B1 && (i & 1) && i / 2 < MT)
+                            fb1[i / 2] = *reinterpret_cast<const bf16x8*>(rbx[P][1] + 16 * RB * (i / 2));
+                        if constexpr (i > B1 && i < B2 && (i - B1 - 1) % 3 == 0 && (i - B1 - 1) / 3 < NT) {
+                            constexpr int r = (i - B1 - 1) / 3;
+                            fa1[r] = *reinterpret_cast<const bf16x8*>(rbw[P][1] + hb_wrow(r, MODE == kSwiglu, WN) * RB);
+                        }
+                        if constexpr (i >= B3 && (i - B3) % RSP == 0 && (i - B3) / RSP < NT + MT) {
+                            constexpr int r = (i - B3) / RSP;  // fa[0], fb[0..MT-1], fa[1..NT-1]
+                            if constexpr (r == 0) fa0[0] = *reinterpret_cast<const bf16x8*>(rbw[1 - P][0]);
+                            else if constexpr (r <= MT)
+                                fb0[r - 1] = *reinterpret_cast<const bf16x8*>(rbx[1 - P][0] + 16 * RB * (r - 1));
+                            else
+                                fa0[r - MT] = *reinterpret_cast<const bf16x8*>(
+                                    rbw[1 - P][0] + hb_wrow(r - MT, MODE == kSwiglu, WN) * RB);
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+                    };
+                    lg_static_for(slot, std::make_integer_sequence<int, 2 * MFK>{});
+                };
+                for (int j = 0; j < NS; j += 2) {
+                    half(std::integral_constant<int, 0>{}, j);
+                    if (j + 1 < NS) half(std::integral_constant<int, 1>{}, j + 1);
+                }
+            } else
+            for (int j = 0; j < NS; ++j) {
+                const unsigned char* cwb = smem + (j & 1) * STAGE;        // slab j (W image, x image at + WIMG)
+                const unsigned char* nwb = smem + ((j + 1) & 1) * STAGE;  // slab j+1
+                const uint32_t dbase = (uint32_t)(uintptr_t)(smem + (j & 1) * STAGE);  // slab j+2 lands here
+                const int kb = min(j + 2, NS1) * RB;
+                // one MFMA slot of the slab, everything decided at compile time
+                auto slot = [&](auto IC) {
+                    constexpr int i = decltype(IC)::value;
+                    if constexpr (i == B1 || i == B2) {
+                        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), visible to hipcc's wait bookkeeping
+                        lg_bar();
+                    }
+                    if constexpr (i == B3) {
+                        lg_vmcnt<(HBV & 2) ? 13 : NPER>();  // (the pieces this wave issued since the last B3)
+                        lg_bar();
+                    }
+                    if constexpr ((HBV & 4) && i == 2 * MFK - 1) __builtin_amdgcn_s_waitcnt(0xC07F);
+                    constexpr int piece = (HBV & 2) ? hb_piece_lib(i, B1, B2, B3, NPW, NPX)
+                                                    : hb_piece(i, B1, B2, B3, DX, DW, NPW, NPX);
+                    // a wave's pieces of one operand are consecutive 8-row groups of the source (the chunk swizzle
+                    // depends on lane / 8 only): one VGPR offset per operand, the piece's rows in the scalar offset
+                    if constexpr (piece >= 0)
+                        lg_dma16_asm<!(HBV & 1)>(piece < NPW ? (const void*)a.w : (const void*)a.x, piece < NPW ? wbytes : xbytes,
+                                     (uint32_t)__builtin_amdgcn_readfirstlane((int)(dbase + dsto[piece])),
+                                     piece < NPW ? voff[0] : voff[NPW],
+                                     kb + (piece < NPW ? piece : piece - NPW) * pstride);
+                    constexpr int ii = i % MFK, s = ii / MT, t = ii % MT;
+                    if constexpr (i < MFK)
+                        acc[s][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0[s], fb0[t], acc[s][t], 0, 0, 0);
+                    else
+                        acc[s][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa1[s], fb1[t], acc[s][t], 0, 0, 0);
+                    if constexpr (i < B1 && (i & 1) && i / 2 < MT)
+                        fb1[i / 2] = *reinterpret_cast<const bf16x8*>(cwb + WIMG + (xrow0 + 16 * (i / 2)) * RB + loff[1]);
+                    if constexpr (i > B1 && i < B2 && (i - B1 - 1) % 3 == 0 && (i - B1 - 1) / 3 < NT) {
+                        constexpr int r = (i - B1 - 1) / 3;
+                        fa1[r] = *reinterpret_cast<const bf16x8*>(cwb + wrow0[r] * RB + loff[1]);
+                    }
+                    if constexpr (i >= B3) {
+                        constexpr int r = i - B3;  // fa[0], fb[0..MT-1], fa[1..NT-1]
+                        if constexpr (r == 0) fa0[0] = *reinterpret_cast<const bf16x8*>(nwb + wrow0[0] * RB + loff[0]);
+                        else if constexpr (r <= MT)
+                            fb0[r - 1] =
+                                *reinterpret_cast<const bf16x8*>(nwb + WIMG + (xrow0 + 16 * (r - 1)) * RB + loff[0]);
+                        else fa0[r - MT] = *reinterpret_cast<const bf16x8*>(nwb + wrow0[r - MT] * RB + loff[0]);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                };
+                lg_static_for(slot, std::make_integer_sequence<int, 2 * MFK>{});
+            }
+            pin_acc();
+        }
         if constexpr (MAN) {
             for (int j = 0; j < NS; ++j) {
                 kstep_man(std::integral_constant<bool, false>{}, fa0, fb0, j, 1, fa1, fb1, 0);
@@ -432,7 +651,7 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
                 __builtin_amdgcn_sched_barrier(0);
             }
         };
-        if constexpr (MAN) {
+        if constexpr (MAN || HB) {
         } else if constexpr (STG) {
             if (grp == 0) loop_stg(std::integral_constant<int, 0>{});
             else loop_stg(std::integral_constant<int, 1>{});
@@ -569,8 +788,109 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
     }  // ring schedule
     lg_vmcnt<0>();  // the past-the-end DMAs must land before the workgroup's LDS is released
 
+    if constexpr (HB && (HBV & 16)) {
+        // ---- staged epilogue (HB bit 4): the wave's bf16 results go through its own 32 KiB of the (now free) LDS
+        // ring, so every global store is a 16-B-per-lane piece of whole 128-B lines (32 dwordx4 stores per lane instead
+        // of 64 dwordx2 ones covering 32-B segments); the residual form reads its residual the same way.  Register
+        // phase: lane (row r = 16 u + lane % 16, columns 16 s + 4 (lane / 16) .. +3) writes 8 B into row r of the
+        // image at 16-B chunk c ^ (r % chunks-per-row) (conflict-free ds_write_b64); store phase: 16 (8 SwiGLU) lanes
+        // per row, one chunk each.
+        constexpr int NCH0 = (MODE == kSwiglu ? WN / 4 : WN / 2) * 2 / 16, RPI0 = 64 / NCH0, NK = XM / 2 / RPI0;
+        // kResid: the residual tile's loads go out first (16 B per lane, whole lines), so their latency hides behind
+        // the staging; the store phase only waits for them
+        u16x8 rvp[MODE == kResid ? NK : 1];
+        if constexpr (MODE == kResid) {
+            const int c = lane % NCH0;
+#pragma unroll
+            for (int k = 0; k < NK; ++k) {
+                const int m = min(m0 + xrow0 + RPI0 * k + lane / NCH0, M - 1);
+                rvp[k] = *reinterpret_cast<const u16x8*>(a.resid + (int64_t)m * a.N + tn * WN + wi * (WN / 2) + c * 8);
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);
+        lg_bar();  // every wave's DMA landed and fragment reads done: the ring is free
+        unsigned char* stg = smem + wave * 32768;
+        const float* inv = reinterpret_cast<const float*>(smem + EXTRA + 16);
+        constexpr int OC = MODE == kSwiglu ? WN / 4 : WN / 2;  // output columns per wave (64 / 128)
+        constexpr int RBY = OC * 2, NCH = RBY / 16;             // image row bytes, 16-B chunks per row
+#pragma unroll
+        for (int u = 0; u < MT; ++u) {
+            const int r = 16 * u + (lane & 15);
+            float sc = 1.f;
+            if constexpr (NORMP) sc = inv[xrow0 + r];
+#pragma unroll
+            for (int s = 0; s < (MODE == kSwiglu ? NT / 2 : NT); ++s) {
+                u16x4 o;
+                if constexpr (MODE == kSwiglu) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const float gv = bf2f(f2bf(acc[s][u][i] * sc));
+                        const float sg = bf2f(f2bf(gv / (1.f + __expf(-gv))));
+                        o[i] = f2bf(sg * bf2f(f2bf(acc[s + NT / 2][u][i] * sc)));
+                    }
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) o[i] = f2bf(acc[s][u][i] * sc);
+                }
+                const int cl = 16 * s + 4 * (lane >> 4);  // first output column of the 4
+                *reinterpret_cast<u16x4*>(stg + r * RBY + (((cl >> 3) ^ (r % NCH)) << 4) + ((cl >> 2) & 1) * 8) = o;
+            }
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // (own region: the wave reads back only what it wrote)
+        constexpr int RPI_ = 64 / NCH;         // image rows per store instruction
+        static_assert(RPI_ == RPI0 && NCH == NCH0, "staging geometry");
+        const int c = lane % NCH;
+        float ssr[MODE == kResid ? NK : 1];  // kResid: this lane's partial of row RPI_ k + lane / NCH
+#pragma unroll
+        for (int k = 0; k < NK; ++k) {
+            const int r = RPI_ * k + lane / NCH;
+            const int m = m0 + xrow0 + r;
+            const u16x8 v = *reinterpret_cast<const u16x8*>(stg + r * RBY + ((c ^ (r % NCH)) << 4));
+            if constexpr (MODE == kSwiglu) {
+                if (m < M) *reinterpret_cast<u16x8*>(a.y + (int64_t)m * a.F + tn * (WN / 2) + wi * OC + c * 8) = v;
+            } else if constexpr (MODE == kResid) {
+                const int n = tn * WN + wi * OC + c * 8;
+                float ss = 0.f;
+                const u16x8 rv = rvp[k];
+                u16x8 o;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const float y = bf2f(f2bf(bf2f(v[i]) + bf2f(rv[i])));
+                    o[i] = f2bf(y);
+                    ss += y * y;
+                }
+                if (m < M) *reinterpret_cast<u16x8*>(a.y + (int64_t)m * a.N + n) = o;
+                ssr[k] = ss;  // (the row's 16 lanes: summed below)
+            } else {
+                const int n = tn * WN + wi * OC + c * 8;
+                if (m < M) {
+                    if (n + 8 <= a.N) *reinterpret_cast<u16x8*>(a.y + (int64_t)m * a.N + n) = v;
+                    else if (n < a.N) *reinterpret_cast<u16x4*>(a.y + (int64_t)m * a.N + n) = u16x4{v[0], v[1], v[2], v[3]};
+                }
+            }
+        }
+        if constexpr (MODE == kResid) {
+            // the RMSNorm partial of each of the wave's 128 rows over its WN / 2 columns: the lanes' partials go to
+            // the wave's image region (read out by now), [row][16], and lane l sums rows l and l + 64
+            float* ssl = reinterpret_cast<float*>(stg);
+#pragma unroll
+            for (int k = 0; k < NK; ++k) ssl[(RPI_ * k + lane / NCH) * 16 + c] = ssr[k];
+            __builtin_amdgcn_s_waitcnt(0xC07F);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int r = lane + 64 * h;
+                const f32x4* q = reinterpret_cast<const f32x4*>(ssl + r * 16);
+                const f32x4 t = (q[0] + q[1]) + (q[2] + q[3]);
+                const float ss = (t[0] + t[1]) + (t[2] + t[3]);
+                const int m = m0 + xrow0 + r;
+                if (m < M) a.part_out[(int64_t)m * (a.N / (WN / 2)) + tn * 2 + wi] = ss;
+            }
+        }
+        return;
+    }
+
     // ---- split-K: fp32 slab in register order, ticket, the last arriver sums every slab in slice order
-    if (S > 1) {
+    if (!HB && S > 1) {  // (HB: no split-K; its fp32 slab code doubles the kernel's register pressure)
         // slab hand-off: plain stores + agent release / acquire fences (each a write-back / invalidate of the XCD's
         // L2), or write-through stores + agent-scope loads with no fence (gemm_skinny.hip's form).  Write-through
         // wins on the 8-16 KB slabs of the 32/64-row tiles (O M = 128 cfg39 split-K 2: 17.5 vs 20.1 us) and loses
@@ -807,7 +1127,17 @@ void lg_launch(const PPArgs& a, hipStream_t st) {
     X(77, 192, 128, 128, 3, 2)     \
     X(78, 128, 32, 128, 7, 2)      \
     X(79, 64, 32, 128, 12, 2)      \
-    X(80, 256, 256, 128, 2, 4, 3)
+    X(80, 256, 256, 128, 2, 4, 3)  \
+    X(81, 256, 256, 128, 2, 2, 4)  \
+    X(82, 256, 256, 128, 2, 2, 5)  \
+    X(83, 256, 256, 128, 2, 2, 6)  \
+    X(84, 256, 256, 128, 2, 2, 8)  \
+    X(85, 256, 256, 128, 2, 2, 7)  \
+    X(86, 256, 256, 128, 2, 2, 13) \
+    X(87, 256, 256, 128, 2, 2, 15) \
+    X(88, 256, 256, 128, 2, 2, 29) \
+    X(89, 256, 256, 128, 2, 2, 31) \
+    X(90, 256, 256, 128, 2, 2, 60)
 
 template <int MODE, bool NORMP>
 bool lg_mode(int cfg, const PPArgs& a, hipStream_t st) {
@@ -871,6 +1201,8 @@ int gemm_lg_xm(int cfg) {
         default: return 0;
     }
 }
+bool gemm_lg_splitk_ok(int cfg) { return cfg < 81 || cfg > 90; }
+
 int gemm_lg_wn(int cfg) {
     if (gemm_lg_ablations_built() && cfg >= 40 && cfg < 72) return 256;
     switch (cfg) {

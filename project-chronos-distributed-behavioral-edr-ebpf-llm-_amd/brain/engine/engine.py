@@ -661,6 +661,7 @@ class Engine:
             self.blocks.release(r.blocks)
             r.blocks = []
             self.stats["completed"] += 1
+            self.stats["generated_tokens"] += len(r.out_ids)
             self._deferred.append((r, "stop" if stop else "length"))
             return
         on_tok = r.meta.get("on_tokens")
@@ -683,6 +684,7 @@ class Engine:
         r.blocks = []
         r.prompt_ids = ctx
         r.resume_out = r.resume_out + out
+        r.meta.setdefault("orig_num_predict", r.num_predict)
         r.num_predict -= n
         r.start_state = -2 - st if st <= -2 else st
         r.prefilled = 0
@@ -1110,6 +1112,12 @@ class Engine:
             self._finish(r, reason, timed=False)
         return [r for r, _ in out]
 
+    def _note_jump(self, r: Request, n0: int, k: int) -> None:
+        r.meta.setdefault("jump_spans", []).append((len(r.resume_out) + n0, k))
+        r.meta["jump_seq"] = self._snap_seq  # every snapshot queued so far predates this jump
+        self.stats["jumps"] += 1
+        self.stats["jump_tokens"] += k
+
     def _jump(self, parked, st, nout, outs) -> dict:
         """Append the grammar-forced token run of every parked row (sampler.hip parks a row entering a state with a
         run).  Each row's pending token and its run go through ONE prefill-mode forward (paged KV at their positions,
@@ -1131,11 +1139,8 @@ class Engine:
                 self.stats["jump_refused"] += 1
                 continue
             ids = outs[s, :n0].tolist() + list(run)
-            r.meta.setdefault("jump_spans", []).append((len(r.resume_out) + n0, k))
-            r.meta["jump_seq"] = self._snap_seq  # every snapshot queued so far predates this jump
-            self.stats["jumps"] += 1
-            self.stats["jump_tokens"] += k
             if end == DONE:
+                self._note_jump(r, n0, k)
                 ended[s] = ids
             else:
                 rows.append((r, ids, end, n0, k))
@@ -1147,6 +1152,8 @@ class Engine:
             # the forward writes positions pos0 .. pos0 + k: grow (preempting the newest rows if the pool is short)
             self._ensure_kv([(r, len(r.prompt_ids) + n0 + k) for r, _, _, n0, k in rows])
             rows = [x for x in rows if self.running.get(x[0].slot) is x[0]]
+        for r, _, _, n0, k in rows:  # (recorded only for rows still running: a preempted row's jump never ran)
+            self._note_jump(r, n0, k)
         if not rows:
             return ended
         pos0 = [len(r.prompt_ids) + n0 - 1 for r, _, _, n0, _ in rows]
@@ -1168,7 +1175,7 @@ class Engine:
         self.s_ctx[sl] = i32([p + k + 1 for p, (*_, k) in zip(pos0, rows)])
         self.s_state[sl] = i32([end for _, _, end, _, _ in rows])
         for p, (r, *_, k) in zip(pos0, rows):
-            r.pos_hi = p + k
+            r.pos_hi = p + k + 1  # the run ends at p + k; the sampler's next token is written one past it
         self.s_row.fill_(-1)
         self.s_row[sl] = i32(list(range(len(rows))))
         ops.constrained_sample(logits, self.s_row, self.bank.next, self.bank.dist, DONE, self.s_state, self.s_rem,
@@ -1213,6 +1220,7 @@ class Engine:
     def _finish(self, req: Request, reason: str, timed: bool = True) -> None:
         if req.orig_plen >= 0:  # preempted at least once: the prompt carried the generated ids while it re-prefilled
             req.prompt_ids = req.prompt_ids[:req.orig_plen]
+            req.num_predict = req.meta.pop("orig_num_predict", req.num_predict)
             if not req.out_ids and req.resume_out:
                 req.out_ids = list(req.resume_out)
         req.done_reason = reason

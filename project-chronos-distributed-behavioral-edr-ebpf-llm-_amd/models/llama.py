@@ -721,7 +721,7 @@ class LlamaModel:
         layer by layer on the compute stream while every row-parallel projection's all-reduce — the fused IPC one-shot
         + residual add + RMSNorm — runs on a second stream (``self._comm``), ordered by events:
 
-            compute: attn(A) | attn(B) | wait ARo(A) mlp(A) | wait ARo(B) mlp(B) | wait ARd(A) attn'(A) ...
+            compute: attn(A) | attn(B) | wait ARo(A) mlp(A) | wait ARo(B) mlp(B) | wait ARd(A) attn'(A) | wait ARd(B) ..
             comm:            ARo(A)   ARo(B)               ARd(A)             ARd(B)
 
         so half A's all-reduce hides behind half B's compute and vice versa.  All all-reduces share ONE stream, issued
@@ -755,19 +755,29 @@ class LlamaModel:
             st["x"] = self._norm(h, st, w.layers[0].attn_norm, first=True)
             states.append(st)
         L = len(w.layers)
+        # each half waits for its own previous down all-reduce only right before its next attention, so half B's
+        # down all-reduce runs beside half A's next attention (and half A's beside half B's MLP)
+        pend_d = [None] * len(states)
         for li, lw in enumerate(w.layers):
-            pend = [ar_norm(st, self._attn(li, lw, st, kv), lw.mlp_norm) for st in states]
-            pend2 = []
-            for st, (x, done, _) in zip(states, pend):
+            pend = []
+            for i, st in enumerate(states):
+                if pend_d[i] is not None:
+                    x, done, _ = pend_d[i]
+                    main.wait_event(done)
+                    st["x"] = x
+                    pend_d[i] = None
+                pend.append(ar_norm(st, self._attn(li, lw, st, kv), lw.mlp_norm))
+            for i, (st, (x, done, _)) in enumerate(zip(states, pend)):
                 main.wait_event(done)
                 st["x"] = x
                 nxt = w.layers[li + 1].attn_norm if li + 1 < L else w.norm
-                pend2.append(ar_norm(st, self._mlp(lw, st), nxt))
+                pend_d[i] = ar_norm(st, self._mlp(lw, st), nxt)
             del pend
-            for st, (x, done, _) in zip(states, pend2):
-                main.wait_event(done)
-                st["x"] = x
-            del pend2
+        for i, st in enumerate(states):
+            x, done, _ = pend_d[i]
+            main.wait_event(done)
+            st["x"] = x
+        del pend_d
         logits = ops.linear(torch.cat([st["x"] for st in states]), w.lm_head)
         logits = tp.all_gather_last(logits)
         return logits if logits.dtype == logits_dtype else logits.to(logits_dtype)

@@ -34,14 +34,19 @@ PP_PLAIN, PP_SWIGLU, PP_RESID = 0, 1, 2
 # x rows (BM) / W rows (BN) per tile.  0-11: gemm_pp.hip (ping-pong); 12-35: gemm_lg.hip (software-pipelined: 12-19 and
 # 29-31 the ring schedule, 20-28 the 64-deep slab schedule, 32-39 mid-M weight streaming with 64 W rows, 72-75 the
 # same for M <= 32 with 32-row x tiles; 76-77 192 W rows x 128 x rows; 78-79 32-row x tiles with 7 / 12-stage rings;
-# 80 = 20 on 32x32x16 MFMAs)
+# 80 = 20 on 32x32x16 MFMAs; 81-89 the 4-wave HB slab loop, 256 x 256 tiles, no split-K: 86 / 87 precomputed addressing
+# (87: hipBLASLt's DMA distribution), 88 / 89 the same + the LDS-staged epilogue, 90 = 88 with the next slab's
+# fragment reads from MFMA 94)
 _PP_BM = {0: 256, 1: 128, 2: 256, 3: 128, 4: 256, 5: 128, 6: 256, 7: 128, 8: 256, 9: 128, 10: 256, 11: 128,
           12: 256, 13: 128, 14: 256, 15: 128, 16: 256, 17: 128, 18: 256, 19: 128, 20: 256, 21: 256, 22: 128, 23: 128,
           24: 256, 25: 128, 26: 256, 27: 128, 28: 128, 29: 128, 30: 256, 31: 128, 32: 128, 33: 64, 34: 128, 35: 256,
-          36: 64, 37: 128, 38: 64, 39: 64, 72: 32, 73: 32, 74: 32, 75: 32, 76: 128, 77: 128, 78: 32, 79: 32, 80: 256}
+          36: 64, 37: 128, 38: 64, 39: 64, 72: 32, 73: 32, 74: 32, 75: 32, 76: 128, 77: 128, 78: 32, 79: 32, 80: 256,
+          **{c: 256 for c in range(81, 91)}}
 _PP_BN = {0: 256, 1: 256, 2: 128, 3: 128, 4: 256, 5: 256, 6: 128, 7: 128, 8: 256, 9: 256, 10: 128, 11: 128,
           12: 256, 13: 256, 14: 128, 15: 128, 16: 256, 17: 256, 18: 128, 19: 128, 20: 256, 21: 256, 22: 256, 23: 128,
-          24: 256, 25: 256, 26: 256, 27: 256, 28: 128, 29: 256, 30: 128, 31: 128, 32: 64, 33: 64, 34: 64, 35: 64, 36: 64, 37: 64, 38: 128, 39: 64, 72: 64, 73: 128, 74: 64, 75: 128, 76: 192, 77: 192, 78: 128, 79: 64, 80: 256}
+          24: 256, 25: 256, 26: 256, 27: 256, 28: 128, 29: 256, 30: 128, 31: 128, 32: 64, 33: 64, 34: 64, 35: 64, 36: 64, 37: 64, 38: 128, 39: 64, 72: 64, 73: 128, 74: 64, 75: 128, 76: 192, 77: 192, 78: 128, 79: 64, 80: 256,
+          **{c: 256 for c in range(81, 91)}}
+HB_FIRST, HB_LAST = 81, 90  # gemm_lg.hip HB configs: no split-K path
 LG_FIRST = 12  # first gemm_lg.hip config: kResid partials every BN/2 columns (gemm_pp: BN/4)
 # relative per-CU MAC rate of each tile config at full occupancy (gate_up M = 1024 / 16384 sweeps, profiles/r3_gemm_pp_*,
 # profiles/r4_gemm_lg_*)
@@ -49,7 +54,8 @@ _PP_RATE = {0: 1.0, 1: 0.84, 2: 0.84, 3: 0.66, 4: 1.0, 5: 0.71, 6: 0.73, 7: 0.6,
             12: 0.95, 13: 0.7, 14: 0.7, 15: 0.75, 16: 0.98, 17: 0.7, 18: 0.7, 19: 0.75, 20: 1.05, 21: 0.7, 22: 0.7,
             23: 0.75, 24: 1.1, 25: 0.8, 26: 1.1, 27: 0.8, 28: 0.75, 29: 0.8, 30: 0.8, 31: 0.75, 32: 0.5,
             33: 0.4, 34: 0.5, 35: 0.55, 36: 0.4, 37: 0.5, 38: 0.5, 39: 0.4, 72: 0.3,
-            73: 0.3, 74: 0.3, 75: 0.3, 76: 0.75, 77: 0.7, 78: 0.3, 79: 0.3, 80: 1.05}
+            73: 0.3, 74: 0.3, 75: 0.3, 76: 0.75, 77: 0.7, 78: 0.3, 79: 0.3, 80: 1.05,
+            **{c: 1.15 for c in range(81, 91)}}
 # skinny-M configs (gemm_skinny.hip SK_CONFIGS): plan id SK_BASE + c -> (RT: W tiles of 16 rows, MT: M <= 16 MT,
 # NW: waves splitting K inside the workgroup)
 SK_BASE = 100
@@ -133,7 +139,7 @@ def _pp_valid(cfg: int, n: int, k: int, mode: int, sk: int, m: int = 0) -> bool:
     if cfg >= SK_BASE:
         return cfg - SK_BASE in _SK and _sk_valid(cfg - SK_BASE, m, n, k, mode, sk)
     bn = _PP_BN[cfg]
-    if k % 64 or (k // 64) % sk:
+    if k % 64 or (k // 64) % sk or (HB_FIRST <= cfg <= HB_LAST and sk != 1):
         return False
     return n % 4 == 0 if mode == PP_PLAIN else n % bn == 0
 
