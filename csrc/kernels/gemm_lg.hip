@@ -304,15 +304,20 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
 #pragma unroll
         for (int t = 0; t < MT; ++t) acc[s][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // NORMP: the producer's partials of the tile's x rows, all loads issued before the DMA prologue
+    // NORMP: the producer's partials of the tile's x rows, all loads issued before the DMA prologue.  Lane l < RPW
+    // of wave w owns local row w RPW + l and sums that row's partials itself (16-B loads of up to 64 partials, the
+    // rest in a tail loop): no cross-lane reduction (the per-row wave_sum of 6 shuffles cost the 4-wave 256-row tiles
+    // 64 dependent reductions per wave before the first MFMA)
     constexpr int RPW = XM / NW;  // x rows per wave for the inv computation
-    float pv[NORMP ? RPW : 1];
+    static_assert(RPW <= 64, "one x row per lane");
+    f32x4 pv4[NORMP ? 16 : 1];
+    const int prow = wave * RPW + lane;  // (lanes >= RPW: a clamped duplicate row, never written)
+    const bool pv_vec = NORMP && (a.nparts_in & 3) == 0;
     if constexpr (NORMP) {
+        const float* pp = a.part_in + (int64_t)min(m0 + min(prow, XM - 1), M - 1) * a.nparts_in;
 #pragma unroll
-        for (int j = 0; j < RPW; ++j) {
-            const int m = min(m0 + wave + NW * j, M - 1);
-            pv[j] = lane < a.nparts_in ? a.part_in[(int64_t)m * a.nparts_in + lane] : 0.f;
-        }
+        for (int i = 0; i < 16; ++i)
+            pv4[i] = pv_vec && 4 * i < a.nparts_in ? *reinterpret_cast<const f32x4*>(pp + 4 * i) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 
     // ---- prologue: stages 0 .. ST-2 in flight (slab schedule: slabs 0 and 1)
@@ -323,18 +328,13 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
 
     if constexpr (NORMP) {
         float* inv = reinterpret_cast<float*>(smem + EXTRA + 16);
-        if (a.nparts_in > 64) {
+        const float* pp = a.part_in + (int64_t)min(m0 + min(prow, XM - 1), M - 1) * a.nparts_in;
+        f32x4 t4 = (pv4[0] + pv4[1]) + (pv4[2] + pv4[3]);
 #pragma unroll
-            for (int j = 0; j < RPW; ++j) {
-                const int m = min(m0 + wave + NW * j, M - 1);
-                for (int i = lane + 64; i < a.nparts_in; i += 64) pv[j] += a.part_in[(int64_t)m * a.nparts_in + i];
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < RPW; ++j) {
-            const float ss = wave_sum(pv[j]);
-            if (lane == 0) inv[wave + NW * j] = rsqrtf(ss / (float)K + a.eps);
-        }
+        for (int i = 4; i < 16; i += 4) t4 += (pv4[i] + pv4[i + 1]) + (pv4[i + 2] + pv4[i + 3]);
+        float ss = (t4[0] + t4[1]) + (t4[2] + t4[3]);
+        for (int i = pv_vec ? 64 : 0; i < a.nparts_in; ++i) ss += pp[i];
+        if (lane < RPW) inv[prow] = rsqrtf(ss / (float)K + a.eps);
     }
 
     if constexpr (SLAB) {
@@ -789,6 +789,47 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
     lg_vmcnt<0>();  // the past-the-end DMAs must land before the workgroup's LDS is released
 
     if constexpr (HB && (HBV & 16)) {
+        if (S > 1) {
+            // ---- split-K for the staged HB configs (M <= 2048 shapes whose 256 x 256 tile grid under-fills the chip):
+            // every slice stores its fp32 tile in register order (plain stores + agent release), the last arriver of
+            // the ticket sums all slices' slabs in slice order (deterministic) into its accumulators, one W block at a
+            // time (a compiler barrier per block keeps hipcc from hoisting all 64 slab loads at once), then runs the
+            // staged epilogue below like an unsplit tile
+            float* slab = a.ws + (int64_t)task * (WN * XM);
+#pragma unroll
+            for (int s = 0; s < NT; ++s)
+#pragma unroll
+                for (int u = 0; u < MT; ++u)
+                    *reinterpret_cast<f32x4*>(slab + (((wave * NT + s) * MT + u) * 64 + lane) * 4) = acc[s][u];
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            int* flag = reinterpret_cast<int*>(smem + EXTRA);
+            if (tid == 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const int old = __hip_atomic_fetch_add(a.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const int last = old == S - 1;
+                if (last) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __hip_atomic_store(a.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+                *flag = last;
+            }
+            __syncthreads();
+            if (!*flag) return;
+#pragma unroll
+            for (int s = 0; s < NT; ++s) {
+#pragma unroll
+                for (int u = 0; u < MT; ++u) {
+                    const int64_t e = (((wave * NT + s) * MT + u) * 64 + lane) * 4;
+                    f32x4 t = *reinterpret_cast<const f32x4*>(a.ws + (int64_t)(tile * S) * (WN * XM) + e);
+                    for (int o = 1; o < S; ++o) t += *reinterpret_cast<const f32x4*>(a.ws + (int64_t)(tile * S + o) * (WN * XM) + e);
+                    acc[s][u] = t;
+                }
+                asm volatile("" ::: "memory");
+            }
+        }
         // ---- staged epilogue (HB bit 4): the wave's bf16 results go through its own 32 KiB of the (now free) LDS
         // ring, so every global store is a 16-B-per-lane piece of whole 128-B lines (32 dwordx4 stores per lane instead
         // of 64 dwordx2 ones covering 32-B segments); the residual form reads its residual the same way.  Register
@@ -1201,7 +1242,7 @@ int gemm_lg_xm(int cfg) {
         default: return 0;
     }
 }
-bool gemm_lg_splitk_ok(int cfg) { return cfg < 81 || cfg > 90; }
+bool gemm_lg_splitk_ok(int cfg) { return cfg < 81 || cfg > 90 || cfg == 88 || cfg == 89 || cfg == 90; }
 
 int gemm_lg_wn(int cfg) {
     if (gemm_lg_ablations_built() && cfg >= 40 && cfg < 72) return 256;

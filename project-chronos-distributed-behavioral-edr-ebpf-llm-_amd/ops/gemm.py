@@ -46,7 +46,8 @@ _PP_BN = {0: 256, 1: 256, 2: 128, 3: 128, 4: 256, 5: 256, 6: 128, 7: 128, 8: 256
           12: 256, 13: 256, 14: 128, 15: 128, 16: 256, 17: 256, 18: 128, 19: 128, 20: 256, 21: 256, 22: 256, 23: 128,
           24: 256, 25: 256, 26: 256, 27: 256, 28: 128, 29: 256, 30: 128, 31: 128, 32: 64, 33: 64, 34: 64, 35: 64, 36: 64, 37: 64, 38: 128, 39: 64, 72: 64, 73: 128, 74: 64, 75: 128, 76: 192, 77: 192, 78: 128, 79: 64, 80: 256,
           **{c: 256 for c in range(81, 91)}}
-HB_FIRST, HB_LAST = 81, 90  # gemm_lg.hip HB configs: no split-K path
+HB_FIRST, HB_LAST = 81, 90  # gemm_lg.hip HB configs
+HB_SPLITK = (88, 89, 90)  # ... with the staged epilogue: the only ones with a split-K path
 LG_FIRST = 12  # first gemm_lg.hip config: kResid partials every BN/2 columns (gemm_pp: BN/4)
 # relative per-CU MAC rate of each tile config at full occupancy (gate_up M = 1024 / 16384 sweeps, profiles/r3_gemm_pp_*,
 # profiles/r4_gemm_lg_*)
@@ -139,7 +140,7 @@ def _pp_valid(cfg: int, n: int, k: int, mode: int, sk: int, m: int = 0) -> bool:
     if cfg >= SK_BASE:
         return cfg - SK_BASE in _SK and _sk_valid(cfg - SK_BASE, m, n, k, mode, sk)
     bn = _PP_BN[cfg]
-    if k % 64 or (k // 64) % sk or (HB_FIRST <= cfg <= HB_LAST and sk != 1):
+    if k % 64 or (k // 64) % sk or (HB_FIRST <= cfg <= HB_LAST and sk != 1 and cfg not in HB_SPLITK):
         return False
     return n % 4 == 0 if mode == PP_PLAIN else n % bn == 0
 

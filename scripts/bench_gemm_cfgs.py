@@ -36,6 +36,8 @@ SHAPES = {
     "qkv1k": (1024, 6144, 4096, 0),
     "o1k": (1024, 4096, 4096, 2),
     "down1k": (1024, 4096, 14336, 2),
+    "down2k": (2048, 4096, 14336, 2),
+    "o2k": (2048, 4096, 4096, 2),
 }
 
 
@@ -55,13 +57,17 @@ def t_us(fn, iters=10, rounds=7):
     return statistics.median(out)
 
 
-def lib_fn(x, w, r, mode):
+def lib_fn(x, ws, r, mode, wnext, normp=False):
+    """The library path of the same epilogue (+ the standalone RMSNorm pass the folded-norm kernels save)."""
+    from chronos import ops
+
+    nw = torch.ones(x.shape[1], device=x.device, dtype=x.dtype)
+    xin = (lambda: ops.rmsnorm(x, nw, 1e-5)) if normp else (lambda: x)  # noqa: E731
     if mode == 0:
-        return lambda: x @ w.t()
+        return lambda: xin() @ wnext().t()
     if mode == 1:
-        f = w.shape[0] // 2
-        return lambda: (lambda h: torch.nn.functional.silu(h[:, :f]) * h[:, f:])(x @ w.t())
-    return lambda: x @ w.t() + r
+        return lambda: ops.silu_mul(xin() @ wnext().t())
+    return lambda: x @ wnext().t() + r
 
 
 def main():
@@ -70,6 +76,8 @@ def main():
     ap.add_argument("--shapes", default="sq8192,qkv16k,o16k,gu16k,down16k")
     ap.add_argument("--out", default=None)
     ap.add_argument("--check", type=int, default=1)
+    ap.add_argument("--cold", type=int, default=0, help="1: rotate weight copies over >= 1 GiB (each call meets cold weights)")
+    ap.add_argument("--normp", type=int, default=0, help="1: modes 0/1 with the folded-RMSNorm prologue (the decoder's call)")
     ap.add_argument("--gms", default="", help="comma list of pp_gm tile-group sizes to sweep (knob; default: as set)")
     a = ap.parse_args()
     from chronos import ops
@@ -77,18 +85,30 @@ def main():
     ops.load()
     C = torch.ops.chronos
     dev = "cuda"
-    cfgs = [int(c) for c in a.cfgs.split(",") if c]
+    # "cfg" or "cfg:splitk"
+    cfgs = [tuple(int(v) for v in (c.split(":") + ["1"])[:2]) for c in a.cfgs.split(",") if c]
     fh = open(a.out, "a") if a.out else None
     for name in a.shapes.split(","):
         m, n, k, mode = SHAPES[name]
         g = torch.Generator(device=dev).manual_seed(m + n + k)
         x = torch.randn(m, k, device=dev, generator=g).to(torch.bfloat16)
         w = (torch.randn(n, k, device=dev, generator=g) * 0.02).to(torch.bfloat16)
+        ws = [w] + ([w.clone() for _ in range(max(1, -(-(1 << 30) // (n * k * 2))) - 1)] if a.cold else [])
+        wi = [0]
+
+        def wnext():
+            wi[0] = (wi[0] + 1) % len(ws)
+            return ws[wi[0]]
         r = torch.randn(m, n, device=dev, generator=g).to(torch.bfloat16) if mode == 2 else None
-        rec = {"shape": name, "M": m, "N": n, "K": k, "mode": mode}
+        rec = {"shape": name, "M": m, "N": n, "K": k, "mode": mode, "normp": bool(a.normp and mode != 2)}
+        part = None
+        xs = x.float()
+        if a.normp and mode != 2:  # producer partials of x: 16 per row (any count works), the kernel scales rows
+            part = torch.stack([(xs[:, i::16] ** 2).sum(1) for i in range(16)], 1).contiguous()
+            xs = xs * torch.rsqrt((xs * xs).sum(1, keepdim=True) / k + 1e-5)
         ref = None
         if a.check:
-            h = x.float() @ w.float().t()
+            h = xs @ w.float().t()
             if mode == 1:
                 f = n // 2
                 ref = torch.nn.functional.silu(h[:, :f]) * h[:, f:]
@@ -103,20 +123,21 @@ def main():
             if gm is not None:
                 C.set_knob("pp_gm", gm)
             sfx = "" if gm is None else f"_gm{gm}"
-            for cfg in cfgs:
-                fn = lambda cfg=cfg: C.gemm_pp(x, w, mode, cfg, 1, r, None, 1e-5, False)  # noqa: E731
+            for cfg, sk in cfgs:
+                tag = f"cfg{cfg}" + (f"sk{sk}" if sk > 1 else "")
+                fn = lambda cfg=cfg, sk=sk: C.gemm_pp(x, wnext(), mode, cfg, sk, r, part, 1e-5, False)  # noqa: E731
                 try:
                     y = fn()[0]
                 except RuntimeError as e:  # config not valid at this shape
-                    rec[f"cfg{cfg}"] = str(e).splitlines()[0][:80]
+                    rec[tag] = str(e).splitlines()[0][:80]
                     continue
                 if ref is not None and gm == gms[0]:
-                    rec[f"cfg{cfg}_err"] = round(((y.float() - ref).abs().max() / ref.abs().max()).item(), 5)
+                    rec[f"{tag}_err"] = round(((y.float() - ref).abs().max() / ref.abs().max()).item(), 5)
                 del y
                 us = t_us(fn)
-                rec[f"cfg{cfg}{sfx}_us"] = round(us, 1)
-                rec[f"cfg{cfg}{sfx}_TF"] = round(fl / us / 1e6, 1)
-        lf = lib_fn(x, w, r, mode)
+                rec[f"{tag}{sfx}_us"] = round(us, 1)
+                rec[f"{tag}{sfx}_TF"] = round(fl / us / 1e6, 1)
+        lf = lib_fn(x, ws, r, mode, wnext, part is not None)
         us = t_us(lf)
         rec["lib_us"] = round(us, 1)
         rec["lib_TF"] = round(fl / us / 1e6, 1)
@@ -125,7 +146,7 @@ def main():
         if fh:
             fh.write(line + "\n")
             fh.flush()
-        del x, w, r, ref
+        del x, w, ws, r, ref
         torch.cuda.empty_cache()
 
 

@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 kernel trace of a short headline bench, kept (gzipped) for offline gap analysis.
-# Usage (gpurun): bash scripts/gpu_trace_keep.sh [extra bench args]
+# Usage (gpurun): bash scripts/trace_keep.sh [extra bench args]
 R=${GRAFT_REPO_ROOT:-/root/repo}
 cd "$R" || exit 1
 export TMPDIR=/tmp

@@ -1,7 +1,7 @@
 """GPU time of the TIMED wave of a `bench.py --steps 1 --warmup 1` kernel trace, split by forward kind (decode bucket
 T, prefill chunks) and kernel class, plus the device-idle gaps inside the region (host stalls).
 
-    python scripts/wave_breakdown.py gpurun_out/ktrace_min.csv.gz   (written by scripts/gpu_trace_keep.sh)
+    python scripts/wave_breakdown.py gpurun_out/ktrace_min.csv.gz   (written by scripts/trace_keep.sh)
 """
 import collections
 import csv
