@@ -3,6 +3,12 @@ the engine runs it: a captured hipGraph of the forward, replayed; prints ms per 
 kernels to rocprofv3.  VERDICT r4 item 5 measures the T = 128 bucket (the 70B-TP8 decode shape class).
 
     python scripts/fw_bucket.py --rows 128 [--model llama3-8b] [--ctx 200] [--iters 20]
+    python scripts/fw_bucket.py --model llama3-70b --tp-rank-of 8 --rows 256     # one rank of 70B TP=8
+
+``--tp-rank-of W`` builds rank 0's shard of a W-way tensor-parallel model (column-parallel QKV / gate_up / LM head,
+row-parallel O / down: the plan's TP-shard GEMM shapes, 1/W of the heads for attention) on one GPU and replaces the
+collectives by their local part (all-reduce = identity, the fused all-reduce + residual + RMSNorm = the local add +
+RMSNorm, the logits all-gather = the rank's vocab shard): the per-rank compute of a TP decode step without xGMI.
 """
 import argparse
 import json
@@ -14,6 +20,26 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+def rank_tp(world: int):
+    """Rank 0 of a ``world``-way TP job with its collectives reduced to their local part (see module docstring)."""
+    from chronos.parallel.tp import TPContext
+
+    class RankTP(TPContext):
+        def all_reduce(self, x):
+            return x
+
+        def all_reduce_async(self, x):
+            return x, None
+
+        def all_gather_last(self, x):
+            return x
+
+        def broadcast_obj(self, obj, src=0):
+            return obj
+
+    return RankTP(rank=0, world=world)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="llama3-8b")
@@ -22,6 +48,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--weights", default="bf16", choices=["bf16", "fp8"])
     ap.add_argument("--knob", action="append", default=[], help="kernel knob name=value (torch.ops.chronos.set_knob)")
+    ap.add_argument("--tp-rank-of", type=int, default=1, help="W > 1: one rank of a W-way TP model, local collectives")
     a = ap.parse_args()
     from chronos import ops
     from chronos.models.llama import KVCache, StepBatch, build_model
@@ -31,7 +58,8 @@ def main():
         name, val = kv_.split("=")
         torch.ops.chronos.set_knob(name, int(val))
     dev = torch.device("cuda")
-    m = build_model(a.model, dev, weight_dtype=a.weights)
+    tp = rank_tp(a.tp_rank_of) if a.tp_rank_of > 1 else None
+    m = build_model(a.model, dev, tp=tp, weight_dtype=a.weights)
     n, bs = a.rows, 16
     nbs = (a.ctx + 1 + bs - 1) // bs
     kv = KVCache(m.cfg, m.tp, n * nbs + 1, bs, dev)
@@ -61,7 +89,8 @@ def main():
     torch.cuda.synchronize()
     ms = s.elapsed_time(e) / a.iters
     wbytes = m.w.nbytes()
-    print(json.dumps({"model": a.model, "weights": a.weights, "rows": n, "ctx": a.ctx, "knobs": a.knob,
+    print(json.dumps({"model": a.model, "tp_rank_of": a.tp_rank_of, "weights": a.weights, "rows": n, "ctx": a.ctx,
+                      "knobs": a.knob,
                       "ms_per_forward": round(ms, 3),
                       "weight_GB": round(wbytes / 1e9, 2), "weight_stream_TBps": round(wbytes / ms / 1e9, 2)}))
 

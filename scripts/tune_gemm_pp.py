@@ -88,6 +88,13 @@ def candidates(m, n, k, mode, keep=6):
     # tile grid under-fills the chip
     # (from M = 128: the wide-W-row tiles over the whole x panel, split-K to fill the chip — at mid-M the L2 -> LDS
     # feed, not HBM, bounds the stream, and x bytes per workgroup scale with x rows / W rows)
+    # the HB configs (88 / 89: 4-wave three-barrier slab loop + staged epilogue; split-K only when the grid is small)
+    if m >= 512:
+        for cfg in (88, 89):
+            tiles = -(-m // 256) * -(-n // 256)
+            for sk in (1, 2):
+                if G._pp_valid(cfg, n, k, mode, sk) and (sk == 1 or tiles < 128) and (cfg, sk) not in out:
+                    out.append((cfg, sk))
     if m >= 128:
         for cfg in (20, 80, 29, 30, 19, 31, 23, 76, 77, 22):
             bm, bn = G._PP_BM[cfg], G._PP_BN[cfg]
@@ -138,6 +145,9 @@ def main():
     ap.add_argument("--merge", default="", help="plan file whose rows at M not measured in this run are kept")
     ap.add_argument("--ops", default="", help="only these projections (e.g. qkv,lm_head)")
     ap.add_argument("--fp8", action="store_true", help="tune the W8A8 fp8 routing (qplans) instead of the bf16 plan")
+    ap.add_argument("--own-only", action="store_true",
+                    help="route the fastest hand-written candidate even where the library is faster (its margin is "
+                         "still recorded in the table)")
     args = ap.parse_args()
     merged = {}
     if args.merge:
@@ -218,7 +228,7 @@ def main():
                         times[c].append(st.elapsed_time(en) * 1000 / iters)
                 best = min(cands, key=lambda c: min(times[c]))
                 lib_us, own_us = min(times["lib"]), min(times[best])
-                use_lib = lib_us < own_us / 1.03
+                use_lib = lib_us < own_us / 1.03 and not args.own_only
                 if m > 1:
                     rows.append([m, -1 if use_lib else best[0], 1 if use_lib else best[1]])
                 wbytes = n * k * 2
