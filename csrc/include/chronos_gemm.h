@@ -44,7 +44,7 @@ bool gemm_lg_splitk_ok(int cfg);  // false for the HB configs (VAR 4): no split-
 bool gemm_lg_ablations_built();  // the timing-only ablation ids 40-71 exist (CHRONOS_GEMM_ABLATIONS build)
 bool launch_gemm_lg(int cfg, int mode, bool normp, const PPArgs& a, hipStream_t st);
 // W8A8 fp8 configs of the same kernel (ring schedule, 128-deep stages; a.kts counts 128-deep units), own id space
-constexpr int kLGF8Configs = 4;
+constexpr int kLGF8Configs = 5;
 int gemm_lg_f8_xm(int cfg);
 int gemm_lg_f8_wn(int cfg);
 bool launch_gemm_lg_f8(int cfg, bool swiglu, const PPArgs& a, hipStream_t st);

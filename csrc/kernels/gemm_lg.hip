@@ -101,6 +101,16 @@ __device__ __forceinline__ void lg_dma16_asm(const void* base, int bytes, uint32
 
 // HB: image row of W fragment block s relative to block 0 (SwiGLU: gate blocks 0 .. 3, then the up blocks at WN / 2)
 constexpr int hb_wrow(int s, bool swiglu, int WN) { return swiglu ? (s < 4 ? 16 * s : WN / 2 + 16 * (s - 4)) : 16 * s; }
+// ... of 32-row block S (F8HB)
+constexpr int hb_wrow32(int S, bool swiglu, int WN) { return swiglu ? (S < 2 ? 32 * S : WN / 2 + 32 * (S - 2)) : 32 * S; }
+// F8HB slab schedule (32 MFMA slots): x pieces spread over [B1, B2), W pieces over [B2, B3)
+constexpr int hb8_piece(int i, int B1, int B2, int B3, int NPW, int NPX) {
+    for (int p = 0; p < NPX; ++p)
+        if (B1 + p * (B2 - B1) / NPX == i) return NPW + p;
+    for (int p = 0; p < NPW; ++p)
+        if (B2 + p * (B3 - B2) / NPW == i) return p;
+    return -1;
+}
 
 // HB slab schedule: the DMA piece issued before MFMA i of the 128 (-1: none).  Pieces 0 .. NPW-1 are W, the rest x.
 constexpr int hb_piece(int i, int B1, int B2, int B3, int DX, int DW, int NPW, int NPX) {
@@ -169,8 +179,13 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
     constexpr bool HB = VAR >= 4 && VAR < 68;
     constexpr int HBV = HB ? VAR - 4 : 0;
     constexpr int ES = F8 ? 1 : 2;  // operand bytes per element
-    static_assert(!F8 || (ST >= 3 && RB == 128 && MODE != kResid && !NORMP && VAR == 0 && ABL == 0),
-                  "fp8: ring schedule, 128-B rows, plain / SwiGLU epilogue");
+    // F8 + HB (VAR with bits 8 and 16: precomputed addressing, staged epilogue): the HB slab loop on
+    // v_mfma_scale_f32_32x32x64_f8f6f4 (F8HB below)
+    static_assert(!F8 || (RB == 128 && MODE != kResid && !NORMP && ABL == 0 &&
+                          (ST >= 3 ? VAR == 0 : (HB && (HBV & 24) == 24 && !(HBV & 2) && !(HBV & 32)))),
+                  "fp8: ring schedule or the HB slab loop, 128-B rows, plain / SwiGLU epilogue");
+    constexpr bool F8HB = F8 && HB;
+    constexpr bool L32 = M32 || F8HB;  // 32x32 accumulator blocks
     using FT = std::conditional_t<F8, lg_i32x8, bf16x8>;  // MFMA operand fragment
     constexpr int NW = 2 * NWX;                       // waves: 2 along W x NWX along x (NWX = 4: two per SIMD)
     constexpr int RPI = 1024 / RB;                    // image rows per LDS-DMA instruction
@@ -190,7 +205,7 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
     static_assert(!STG || (SLAB && NWX == 4), "staggered DMA: slab schedule, two waves per SIMD");
     static_assert(!MAN || SLAB, "issue-ordered k-steps: slab schedule");
     static_assert(!M32 || (SLAB && !F8 && ABL == 0 && NT % 2 == 0 && MT % 2 == 0), "32x32 MFMA: slab schedule, bf16");
-    static_assert(!HB || (SLAB && !F8 && ABL == 0 && NWX == 2 && NT == 8 && MT == 8), "HB: 256 x 256 slab, 4 waves");
+    static_assert(!HB || (SLAB && ABL == 0 && NWX == 2 && NT == 8 && MT == 8), "HB: 256 x 256 slab, 4 waves");
     static_assert(ST >= 3 || (SLAB && RB == 128), "slab schedule: 64-deep (128-B row) slabs");
     static_assert(MODE != kSwiglu || (WN / 4) % 16 == 0, "swiglu: WN/4 gate rows per wave, multiple of 16");
     static_assert(RB == 64 || RB == 128, "stage depth 32 or 64");
@@ -276,8 +291,8 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
     }
     const int xrow0 = wj * (XM / NWX);
     // M32: first W row of each 32-row block (SwiGLU: gate blocks, then the matching up blocks)
-    int wrow32[M32 ? NT / 2 : 1];
-    if constexpr (M32) {
+    int wrow32[L32 ? NT / 2 : 1];
+    if constexpr (L32) {
 #pragma unroll
         for (int S = 0; S < NT / 2; ++S) {
             if constexpr (MODE == kSwiglu)
@@ -320,11 +335,35 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
             pv4[i] = pv_vec && 4 * i < a.nparts_in ? *reinterpret_cast<const f32x4*>(pp + 4 * i) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
 
+    // F8HB: the tile's scales, loaded before the prologue and parked in LDS after the ring ([WN] wsc of the image's W
+    // rows — SwiGLU: gate rows, then up rows — then [XM] xsc), so the epilogue reads them from LDS instead of issuing
+    // dependent global loads between its LDS stores (measured: ~10 us per tile of serialised L2 round trips)
+    constexpr int NSCL = F8HB ? (WN + XM + 128 * NWX - 1) / (128 * NWX) : 1;
+    float scv[NSCL];
+    float* scl = reinterpret_cast<float*>(smem + EXTRA + 16 + XM * 4);
+    if constexpr (F8HB) {
+#pragma unroll
+        for (int q = 0; q < NSCL; ++q) {
+            const int i = tid + q * 128 * NWX;
+            int wr;
+            if constexpr (MODE == kSwiglu)
+                wr = i < WN / 2 ? tn * (WN / 2) + i : a.F + tn * (WN / 2) + (i - WN / 2);
+            else
+                wr = min(tn * WN + i, a.N - 1);
+            scv[q] = i < WN ? a.wsc[wr] : a.xsc[min(m0 + min(i - WN, XM - 1), M - 1)];
+        }
+    }
+
     // ---- prologue: stages 0 .. ST-2 in flight (slab schedule: slabs 0 and 1)
     const int grp = wave >> 2;  // wave group (STG): waves w and w+4 share a SIMD
 #pragma unroll
     for (int p = 0; p < (SLAB ? 2 : ST - 1); ++p)
         if (!(STG && p == 1 && grp == 1)) issue(p);  // (STG: group 1 issues its part of slab 1 in slab 0's k-step A)
+    if constexpr (F8HB) {
+#pragma unroll
+        for (int q = 0; q < NSCL; ++q)
+            if (tid + q * 128 * NWX < WN + XM) scl[tid + q * 128 * NWX] = scv[q];
+    }
 
     if constexpr (NORMP) {
         float* inv = reinterpret_cast<float*>(smem + EXTRA + 16);
@@ -371,8 +410,8 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
             for (int t = 0; t < MT; ++t)
                 fb[t] = *reinterpret_cast<const bf16x8*>(xb + (xrow0 + 16 * t) * RB + loff[kk]);
         };
-        f32x16 acc32[M32 ? NT / 2 : 1][M32 ? MT / 2 : 1];
-        if constexpr (M32) {
+        f32x16 acc32[L32 ? NT / 2 : 1][L32 ? MT / 2 : 1];
+        if constexpr (L32) {
 #pragma unroll
             for (int S = 0; S < NT / 2; ++S)
 #pragma unroll
@@ -380,6 +419,32 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
 #pragma unroll
                     for (int i = 0; i < 16; ++i) acc32[S][U][i] = 0.f;
         }
+        // F8HB fragments (v_mfma_scale_f32_32x32x64_f8f6f4): block S (32 W rows) / U (32 x rows) of the slab's 64-deep
+        // k-step kk; lane (r = lane & 31, hf = lane >> 5) holds k-bytes 64 kk + 32 hf .. +31 of row r, i.e. logical
+        // chunks 4 kk + 2 hf and + 1 of the 128-B image row, each one ds_read_b128 at its XOR-swizzled slot (chunk ^
+        // (r & 7), as the DMA wrote it).  Both operands use the same (half, byte) -> k map.  One base VGPR per
+        // (buffer parity, operand, k-step, half); block offsets are immediates.
+        lg_i32x8 ga0[F8HB ? NT / 2 : 1], gb0[F8HB ? MT / 2 : 1], ga1[F8HB ? NT / 2 : 1], gb1[F8HB ? MT / 2 : 1];
+        const unsigned char* f8b[F8HB ? 2 : 1][2][2][2];
+        if constexpr (F8HB) {
+            const int r = lane & 31, hf = lane >> 5;
+#pragma unroll
+            for (int p = 0; p < 2; ++p)
+#pragma unroll
+                for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const int co = ((4 * kk + 2 * hf + h) ^ (r & 7)) << 4;
+                        f8b[p][0][kk][h] = smem + p * STAGE + (wrow32[0] + r) * RB + co;
+                        f8b[p][1][kk][h] = smem + p * STAGE + WIMG + (xrow0 + r) * RB + co;
+                    }
+        }
+        // one F8HB fragment: parity p, operand op (0 W, 1 x), k-step kk, block row offset off (bytes)
+        auto f8rd = [&](int p, int op, int kk, int off) -> lg_i32x8 {
+            const lg_i32x4 lo = *reinterpret_cast<const lg_i32x4*>(f8b[F8HB ? p : 0][op][kk][0] + off);
+            const lg_i32x4 hi = *reinterpret_cast<const lg_i32x4*>(f8b[F8HB ? p : 0][op][kk][1] + off);
+            return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        };
         auto mm = [&](bf16x8 (&fa)[NT], bf16x8 (&fb)[MT]) {
             if constexpr (M32) {
 #pragma unroll
@@ -411,7 +476,13 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
             lg_vmcnt<NPER>();  // slab 0 landed (slab 1 in flight)
         }
         lg_bar();
-        if constexpr (HB) {
+        if constexpr (F8HB) {
+            ga0[0] = f8rd(0, 0, 0, 0);  // (the loop's set-0 read order: ga[0], gb[*], ga[1..])
+#pragma unroll
+            for (int u = 0; u < MT / 2; ++u) gb0[u] = f8rd(0, 1, 0, 32 * RB * u);
+#pragma unroll
+            for (int s = 1; s < NT / 2; ++s) ga0[s] = f8rd(0, 0, 0, hb_wrow32(s, MODE == kSwiglu, WN) * RB);
+        } else if constexpr (HB) {
             // the order of the loop's set-0 reads (fa[0], fb[*], fa[1..]): the same pending-read state enters the loop
             // from the prologue and from the back edge, so hipcc's waits at the first MFMAs stay counted
             fa0[0] = *reinterpret_cast<const bf16x8*>(smem + wrow0[0] * RB + loff[0]);
@@ -483,13 +554,102 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
             // the accumulators live in AGPRs across the whole loop: pinned at both ends, so the epilogue's VGPR use
             // (resid / SwiGLU / norm-scale forms) cannot make the register allocator shuffle them inside the loop
             auto pin_acc = [&]() {
+                if constexpr (F8HB) {
 #pragma unroll
-                for (int s = 0; s < NT; ++s)
+                    for (int S = 0; S < NT / 2; ++S)
 #pragma unroll
-                    for (int t = 0; t < MT; ++t) asm volatile("" : "+a"(acc[s][t]));
+                        for (int U = 0; U < MT / 2; ++U) asm volatile("" : "+a"(acc32[S][U]));
+                } else {
+#pragma unroll
+                    for (int s = 0; s < NT; ++s)
+#pragma unroll
+                        for (int t = 0; t < MT; ++t) asm volatile("" : "+a"(acc[s][t]));
+                }
             };
             pin_acc();
-            if constexpr (HBV & 8) {
+            if constexpr (F8HB) {
+                // W8A8 on the HB loop: a 128-B slab row is 128 e4m3 k = two 64-deep k-steps of 16
+                // v_mfma_scale_f32_32x32x64_f8f6f4 (4 W x 4 x blocks of 32, each MFMA 4x the issue time of a bf16
+                // 16x16x32), so a slab is 32 MFMA slots with the same per-slab bytes, fragment reads (2 ds_read_b128
+                // per fragment, 32 per slab) and DMA pieces as the bf16 loop's 128, and the same three barriers:
+                //   slots 0-3    : set-1 (k-step 1) x fragments of slab j
+                //   B1 (5)       : lgkmcnt(0) + barrier — x buffer released; x pieces of slab j+2 over [B1, B2)
+                //   6, 8, 10, 12 : set-1 W fragments
+                //   B2 (14)      : W buffer released; W pieces of slab j+2 over [B2, B3)
+                //   B3 (28)      : vmcnt(NPER) + barrier — slab j+1 landed
+                //   28-31        : set-0 fragments of slab j+1, two per slot (ga[0], gb[*], ga[1..])
+                constexpr int MK = (NT / 2) * (MT / 2), F1 = 5, F2 = 14, F3 = 28;
+                static_assert(MK == 16 && F1 >= MT / 2 + 1 && F1 + 1 + 2 * (NT / 2 - 1) < F2 - 1 && F3 + 4 == 2 * MK,
+                              "F8HB schedule");
+                uint32_t m0w[2], m0x[2];
+#pragma unroll
+                for (int p = 0; p < 2; ++p) {
+                    m0w[p] = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uintptr_t)(smem + p * STAGE + dsto[0]));
+                    m0x[p] = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uintptr_t)(smem + p * STAGE + dsto[NPW]));
+                }
+                const uint32_t vw = voff[0], vx = voff[NPW];
+                auto half = [&](auto PC, int j) {
+                    constexpr int P = decltype(PC)::value;  // slab j in buffer P, slab j+1 in 1 - P
+                    const int kb = min(j + 2, NS1) * RB;
+                    const void* bw = (const unsigned char*)a.w + kb;
+                    const void* bx = (const unsigned char*)a.x + kb;
+                    const int nw = wbytes - kb, nx = xbytes - kb;
+                    auto slot = [&](auto IC) {
+                        constexpr int i = decltype(IC)::value;
+                        if constexpr (i == F1 || i == F2) {
+                            __builtin_amdgcn_s_waitcnt(0xC07F);
+                            lg_bar();
+                        }
+                        if constexpr (i == F3) {
+                            lg_vmcnt<NPER>();
+                            lg_bar();
+                        }
+                        constexpr int piece = hb8_piece(i, F1, F2, F3, NPW, NPX);
+                        if constexpr (piece >= 0) {
+                            constexpr bool isW = piece < NPW;
+                            constexpr int q = isW ? piece : piece - NPW;
+                            const uint64_t b = (uint64_t)(isW ? bw : bx);
+                            const lg_i32x4 r = {(int)(uint32_t)b, (int)(uint32_t)(b >> 32), isW ? nw : nx, 0x00020000};
+                            if constexpr (q == 0)
+                                asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds"
+                                             ::"v"(isW ? vw : vx), "s"(r), "s"(isW ? m0w[P] : m0x[P]) : "memory");
+                            else
+                                asm volatile("s_add_u32 m0, m0, 0x400\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds"
+                                             ::"v"(isW ? vw : vx), "s"(r), "s"(q * pstride) : "memory");
+                        }
+                        constexpr int ii = i % MK, S = ii / (MT / 2), U = ii % (MT / 2);
+                        if constexpr (i < MK)
+                            acc32[S][U] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ga0[S], gb0[U], acc32[S][U], 0,
+                                                                                        0, 0, 127, 0, 127);
+                        else
+                            acc32[S][U] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ga1[S], gb1[U], acc32[S][U], 0,
+                                                                                        0, 0, 127, 0, 127);
+                        if constexpr (i < MT / 2) gb1[i] = f8rd(P, 1, 1, 32 * RB * i);
+                        if constexpr (i > F1 && (i - F1 - 1) % 2 == 0 && (i - F1 - 1) / 2 < NT / 2) {
+                            constexpr int s = (i - F1 - 1) / 2;
+                            ga1[s] = f8rd(P, 0, 1, hb_wrow32(s, MODE == kSwiglu, WN) * RB);
+                        }
+                        if constexpr (i >= F3) {
+                            lg_static_for(
+                                [&](auto RC) {
+                                    constexpr int r = 2 * (i - F3) + decltype(RC)::value;  // ga[0], gb[0..3], ga[1..3]
+                                    if constexpr (r == 0) ga0[0] = f8rd(1 - P, 0, 0, 0);
+                                    else if constexpr (r <= MT / 2) gb0[r - 1] = f8rd(1 - P, 1, 0, 32 * RB * (r - 1));
+                                    else
+                                        ga0[r - MT / 2] =
+                                            f8rd(1 - P, 0, 0, hb_wrow32(r - MT / 2, MODE == kSwiglu, WN) * RB);
+                                },
+                                std::make_integer_sequence<int, 2>{});
+                        }
+                        __builtin_amdgcn_sched_barrier(0);
+                    };
+                    lg_static_for(slot, std::make_integer_sequence<int, 2 * MK>{});
+                };
+                for (int j = 0; j < NS; j += 2) {
+                    half(std::integral_constant<int, 0>{}, j);
+                    if (j + 1 < NS) half(std::integral_constant<int, 1>{}, j + 1);
+                }
+            } else if constexpr (HBV & 8) {
                 // precomputed addressing: the slab loop unrolled by two, so each half's LDS buffer is a compile-time
                 // parity; fragment reads from 8 per-lane base VGPRs (parity x operand x k-step) + immediate offsets;
                 // the LDS-DMA destination kept in M0 (one s_mov per operand and slab, then s_add 1 KiB per piece, as
@@ -684,7 +844,7 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
             lg_sched<0, MF, (ABL & 1) ? 0 : NPER, NR>();
             __builtin_amdgcn_sched_barrier(0);
         }
-        if constexpr (M32) {
+        if constexpr (L32) {
             // 32x32 accumulator register 4 g + i -> acc[2 S + (g >> 1)][2 U + (g & 1)][i]
 #pragma unroll
             for (int S = 0; S < NT / 2; ++S)
@@ -854,26 +1014,59 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
         const float* inv = reinterpret_cast<const float*>(smem + EXTRA + 16);
         constexpr int OC = MODE == kSwiglu ? WN / 4 : WN / 2;  // output columns per wave (64 / 128)
         constexpr int RBY = OC * 2, NCH = RBY / 16;             // image row bytes, 16-B chunks per row
+        // 16x16 blocks: acc[s][u] covers row 16 u + lane % 16, columns 16 s + 4 (lane / 16) .. +3; L32 (F8HB):
+        // acc[s][u] is 32x32 block (s / 2, u / 2), register group g = 2 (s & 1) + (u & 1): row 32 (u / 2) + lane % 32,
+        // columns 32 (s / 2) + 8 g + 4 (lane / 32) .. +3 (within the wave's OC)
+        static_assert(!F8 || L32, "fp8 HB: 32x32 blocks");
+        auto row_of = [&](int u) { return L32 ? 32 * (u >> 1) + (lane & 31) : 16 * u + (lane & 15); };
+        auto col_of = [&](int s, int u) {
+            return L32 ? 32 * (s >> 1) + 8 * (2 * (s & 1) + (u & 1)) + 4 * (lane >> 5) : 16 * s + 4 * (lane >> 4);
+        };
+        // F8: every scale the register phase needs, loaded up front with clamped indices (no branches, one wait):
+        // per-token xsc of the lane's rows, per-channel wsc of its column groups (SwiGLU: gate and up)
+        constexpr int NSC = MODE == kSwiglu ? NT / 2 : NT;
+        f32x4 c8a[F8 ? NSC : 1][2], c8b[F8 && MODE == kSwiglu ? NSC : 1][2];
+        float xs8[F8 ? MT : 1];
+        if constexpr (F8) {
+#pragma unroll
+            for (int s = 0; s < NSC; ++s)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    c8a[s][h] = *reinterpret_cast<const f32x4*>(scl + wi * OC + col_of(s, h));
+                    if constexpr (MODE == kSwiglu)
+                        c8b[s][h] = *reinterpret_cast<const f32x4*>(scl + WN / 2 + wi * OC + col_of(s, h));
+                }
+#pragma unroll
+            for (int u = 0; u < MT; ++u) xs8[u] = scl[WN + xrow0 + row_of(u)];
+        }
 #pragma unroll
         for (int u = 0; u < MT; ++u) {
-            const int r = 16 * u + (lane & 15);
+            const int r = row_of(u);
             float sc = 1.f;
             if constexpr (NORMP) sc = inv[xrow0 + r];
+            if constexpr (F8) sc = xs8[u];  // per-token scale (rows past M: never stored)
 #pragma unroll
             for (int s = 0; s < (MODE == kSwiglu ? NT / 2 : NT); ++s) {
+                const int cl = col_of(s, u);  // first output column of the lane's 4
                 u16x4 o;
                 if constexpr (MODE == kSwiglu) {
+                    f32x4 cg = {1.f, 1.f, 1.f, 1.f}, cu = {1.f, 1.f, 1.f, 1.f};
+                    if constexpr (F8) {  // per-channel scales of the gate / up rows
+                        cg = c8a[s][u & 1];
+                        cu = c8b[s][u & 1];
+                    }
 #pragma unroll
                     for (int i = 0; i < 4; ++i) {
-                        const float gv = bf2f(f2bf(acc[s][u][i] * sc));
+                        const float gv = bf2f(f2bf(acc[s][u][i] * sc * cg[i]));
                         const float sg = bf2f(f2bf(gv / (1.f + __expf(-gv))));
-                        o[i] = f2bf(sg * bf2f(f2bf(acc[s + NT / 2][u][i] * sc)));
+                        o[i] = f2bf(sg * bf2f(f2bf(acc[s + NT / 2][u][i] * sc * cu[i])));
                     }
                 } else {
+                    f32x4 cw = {1.f, 1.f, 1.f, 1.f};
+                    if constexpr (F8) cw = c8a[s][u & 1];
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) o[i] = f2bf(acc[s][u][i] * sc);
+                    for (int i = 0; i < 4; ++i) o[i] = f2bf(acc[s][u][i] * sc * cw[i]);
                 }
-                const int cl = 16 * s + 4 * (lane >> 4);  // first output column of the 4
                 *reinterpret_cast<u16x4*>(stg + r * RBY + (((cl >> 3) ^ (r % NCH)) << 4) + ((cl >> 2) & 1) * 8) = o;
             }
         }
@@ -882,31 +1075,49 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
         static_assert(RPI_ == RPI0 && NCH == NCH0, "staging geometry");
         const int c = lane % NCH;
         float ssr[MODE == kResid ? NK : 1];  // kResid: this lane's partial of row RPI_ k + lane / NCH
+        // plain / SwiGLU: the image rows are read in batches of SB before their stores (pinned in registers), so
+        // the LDS reads overlap instead of each guarded store waiting for its own read
+        constexpr int SB = MODE == kResid ? 1 : 8;
+        static_assert(NK % SB == 0, "store batches");
 #pragma unroll
-        for (int k = 0; k < NK; ++k) {
-            const int r = RPI_ * k + lane / NCH;
-            const int m = m0 + xrow0 + r;
-            const u16x8 v = *reinterpret_cast<const u16x8*>(stg + r * RBY + ((c ^ (r % NCH)) << 4));
-            if constexpr (MODE == kSwiglu) {
-                if (m < M) *reinterpret_cast<u16x8*>(a.y + (int64_t)m * a.F + tn * (WN / 2) + wi * OC + c * 8) = v;
-            } else if constexpr (MODE == kResid) {
-                const int n = tn * WN + wi * OC + c * 8;
-                float ss = 0.f;
-                const u16x8 rv = rvp[k];
-                u16x8 o;
+        for (int k0 = 0; k0 < NK; k0 += SB) {
+            u16x8 vb[SB];
 #pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    const float y = bf2f(f2bf(bf2f(v[i]) + bf2f(rv[i])));
-                    o[i] = f2bf(y);
-                    ss += y * y;
-                }
-                if (m < M) *reinterpret_cast<u16x8*>(a.y + (int64_t)m * a.N + n) = o;
-                ssr[k] = ss;  // (the row's 16 lanes: summed below)
-            } else {
-                const int n = tn * WN + wi * OC + c * 8;
-                if (m < M) {
-                    if (n + 8 <= a.N) *reinterpret_cast<u16x8*>(a.y + (int64_t)m * a.N + n) = v;
-                    else if (n < a.N) *reinterpret_cast<u16x4*>(a.y + (int64_t)m * a.N + n) = u16x4{v[0], v[1], v[2], v[3]};
+            for (int kk = 0; kk < SB; ++kk) {
+                const int r = RPI_ * (k0 + kk) + lane / NCH;
+                vb[kk] = *reinterpret_cast<const u16x8*>(stg + r * RBY + ((c ^ (r % NCH)) << 4));
+            }
+            if constexpr (SB > 1) {
+#pragma unroll
+                for (int kk = 0; kk < SB; ++kk) asm volatile("" : "+v"(vb[kk]));
+            }
+#pragma unroll
+            for (int kk = 0; kk < SB; ++kk) {
+                const int k = k0 + kk;
+                const int r = RPI_ * k + lane / NCH;
+                const int m = m0 + xrow0 + r;
+                const u16x8 v = vb[kk];
+                if constexpr (MODE == kSwiglu) {
+                    if (m < M) *reinterpret_cast<u16x8*>(a.y + (int64_t)m * a.F + tn * (WN / 2) + wi * OC + c * 8) = v;
+                } else if constexpr (MODE == kResid) {
+                    const int n = tn * WN + wi * OC + c * 8;
+                    float ss = 0.f;
+                    const u16x8 rv = rvp[k];
+                    u16x8 o;
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const float y = bf2f(f2bf(bf2f(v[i]) + bf2f(rv[i])));
+                        o[i] = f2bf(y);
+                        ss += y * y;
+                    }
+                    if (m < M) *reinterpret_cast<u16x8*>(a.y + (int64_t)m * a.N + n) = o;
+                    ssr[k] = ss;  // (the row's 16 lanes: summed below)
+                } else {
+                    const int n = tn * WN + wi * OC + c * 8;
+                    if (m < M) {
+                        if (n + 8 <= a.N) *reinterpret_cast<u16x8*>(a.y + (int64_t)m * a.N + n) = v;
+                        else if (n < a.N) *reinterpret_cast<u16x4*>(a.y + (int64_t)m * a.N + n) = u16x4{v[0], v[1], v[2], v[3]};
+                    }
                 }
             }
         }
@@ -1114,7 +1325,7 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
 
 template <int WN, int XM, int RB, int ST, int MODE, bool NORMP, int NWX, int ABL = 0, int VAR = 0, bool F8 = false>
 void lg_launch(const PPArgs& a, hipStream_t st) {
-    const int lds = ST * (WN + XM) * RB + 16 + XM * 4;
+    const int lds = ST * (WN + XM) * RB + 16 + XM * 4 + (F8 && ST == 2 ? (WN + XM) * 4 : 0);
     auto kern = gemm_lg_kernel<WN, XM, RB, ST, MODE, NORMP, NWX, ABL, VAR, F8>;
     static bool attr = false;
     if (!attr) {
@@ -1256,18 +1467,22 @@ int gemm_lg_wn(int cfg) {
 
 // W8A8 fp8 configs {id, WN, XM, RB, ST, NWX}: ring schedule, one 128-deep v_mfma_scale_f32_16x16x128_f8f6f4 k-step
 // per 128-B stage row (every staged byte carries twice the bf16 kernel's K)
+// 4 (F8HB): the HB slab loop (4 waves, 128 x 128 outputs per wave, three barriers per slab) on
+// v_mfma_scale_f32_32x32x64_f8f6f4, precomputed addressing + LDS-staged epilogue (VAR 29 = bf16 cfg 88's bits)
 #define LG_F8_CONFIGS(X)       \
     X(0, 256, 128, 128, 3, 4)  \
     X(1, 128, 256, 128, 3, 4)  \
     X(2, 128, 128, 128, 4, 2)  \
-    X(3, 128, 128, 128, 3, 4)
+    X(3, 128, 128, 128, 3, 4)  \
+    X(4, 256, 256, 128, 2, 2, 29)
 
 namespace {
+constexpr int lg_f8_var(int v = 0) { return v; }  // (the config's VAR, 0 when the row gives none)
 template <int MODE>
 bool lg_f8_mode(int cfg, const PPArgs& a, hipStream_t st) {
     switch (cfg) {
-#define LG_F8_CASE(ID, WN_, XM_, RB_, ST_, NWX_) \
-    case ID: lg_launch<WN_, XM_, RB_, ST_, MODE, false, NWX_, 0, 0, true>(a, st); return true;
+#define LG_F8_CASE(ID, WN_, XM_, RB_, ST_, NWX_, ...) \
+    case ID: lg_launch<WN_, XM_, RB_, ST_, MODE, false, NWX_, 0, lg_f8_var(__VA_ARGS__), true>(a, st); return true;
         LG_F8_CONFIGS(LG_F8_CASE)
 #undef LG_F8_CASE
         default: return false;
@@ -1277,7 +1492,7 @@ bool lg_f8_mode(int cfg, const PPArgs& a, hipStream_t st) {
 
 int gemm_lg_f8_xm(int cfg) {
     switch (cfg) {
-#define LG_F8_XM(ID, WN_, XM_, RB_, ST_, NWX_) case ID: return XM_;
+#define LG_F8_XM(ID, WN_, XM_, RB_, ST_, NWX_, ...) case ID: return XM_;
         LG_F8_CONFIGS(LG_F8_XM)
 #undef LG_F8_XM
         default: return 0;
@@ -1285,7 +1500,7 @@ int gemm_lg_f8_xm(int cfg) {
 }
 int gemm_lg_f8_wn(int cfg) {
     switch (cfg) {
-#define LG_F8_WN(ID, WN_, XM_, RB_, ST_, NWX_) case ID: return WN_;
+#define LG_F8_WN(ID, WN_, XM_, RB_, ST_, NWX_, ...) case ID: return WN_;
         LG_F8_CONFIGS(LG_F8_WN)
 #undef LG_F8_WN
         default: return 0;

@@ -89,7 +89,8 @@ def _plan_file() -> dict:
 
 
 QLG_BASE = 10  # qplan code >= QLG_BASE: gemm_lg.hip's fp8 config (code - QLG_BASE), row [M, code, split-K]
-QLG_GEO = {0: (128, 256), 1: (256, 128), 2: (128, 128), 3: (128, 128)}  # fp8 config -> (x rows, W rows) per tile
+QLG_GEO = {0: (128, 256), 1: (256, 128), 2: (128, 128), 3: (128, 128),  # fp8 config -> (x rows, W rows) per tile
+           4: (256, 256)}  # 4: the HB slab loop on the 32x32x64 fp8 MFMA (gemm_lg.hip F8HB)
 
 
 def qplan_route(m: int, n: int, k: int, swiglu: bool) -> Optional[tuple[int, int]]:

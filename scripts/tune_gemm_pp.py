@@ -300,7 +300,7 @@ def tune_fp8(args, merged_unused):
             # gemm_lg.hip's fp8 configs (M >= 128): every config that tiles N, split-K while the grid under-fills
             lgc = []
             if m >= 128:
-                for c in range(4):
+                for c in sorted(G_F8):
                     bm, bn = G_F8[c]
                     tiles = -(-m // bm) * (n // bn)
                     for sk in (1, 2, 4):

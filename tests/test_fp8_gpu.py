@@ -159,7 +159,7 @@ def test_fp8_model_tracks_bf16_and_engine_valid():
         assert {"risk_score", "verdict", "reason"} <= set(json.loads(r.text))
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("m,n,k,swiglu,splitk", [(300, 2048, 2048, False, 1), (257, 1024, 4096, True, 1),
                                                  (130, 2052, 1024, False, 2), (77, 512, 2048, True, 4)])
 def test_qgemm_lg(cfg, m, n, k, swiglu, splitk):
@@ -177,7 +177,21 @@ def test_qgemm_lg(cfg, m, n, k, swiglu, splitk):
         torch.testing.assert_close(y.float(), yr.float(), **tol)
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("m,n,k,swiglu", [(300, 512, 128, False), (520, 1024, 1152, True), (600, 776, 1152, False),
+                                          (1, 256, 384, False)])
+def test_qgemm_lg_hb_slab_counts(m, n, k, swiglu):
+    """fp8 config 4 (the HB slab loop on v_mfma_scale_f32_32x32x64_f8f6f4, unrolled by two slabs): one slab, an odd
+    number of slabs, a partial W tile in the staged epilogue, one row."""
+    from chronos.ops import reference as ref
+
+    g = torch.Generator(device=DEV).manual_seed(m + n + k)
+    xq, xs, wq, ws = _qpair(m, n, k, g, swiglu)
+    yr = ref.qlinear(xq, xs, wq, ws, swiglu)
+    y = torch.ops.chronos.qgemm_lg(xq, xs, wq, ws, swiglu, 4, 1)
+    torch.testing.assert_close(y.float(), yr.float(), rtol=2e-2, atol=2e-2 * float(yr.float().abs().mean()) + 1e-6)
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4])
 def test_qgemm_lg_onehot_layout(cfg):
     """One-hot x rows (exact in e4m3): pins the fp8 fragment layout (row, column, k of every lane's 32 bytes)."""
     from chronos.ops import reference as ref
