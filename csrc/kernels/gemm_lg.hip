@@ -978,15 +978,27 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
             }
             __syncthreads();
             if (!*flag) return;
+            // per W block: the MT slab pieces of one slice are loaded together (one round trip per slice and block,
+            // not per piece); the arriving slice's own piece comes from its registers (the same fp32 bits it stored),
+            // so the sum is still slice 0 + 1 + ... in order whoever arrives last
 #pragma unroll
             for (int s = 0; s < NT; ++s) {
+                f32x4 t[MT], v[MT];
+                for (int o = 0; o < S; ++o) {
+                    if (o == ks) {
 #pragma unroll
-                for (int u = 0; u < MT; ++u) {
-                    const int64_t e = (((wave * NT + s) * MT + u) * 64 + lane) * 4;
-                    f32x4 t = *reinterpret_cast<const f32x4*>(a.ws + (int64_t)(tile * S) * (WN * XM) + e);
-                    for (int o = 1; o < S; ++o) t += *reinterpret_cast<const f32x4*>(a.ws + (int64_t)(tile * S + o) * (WN * XM) + e);
-                    acc[s][u] = t;
+                        for (int u = 0; u < MT; ++u) v[u] = acc[s][u];
+                    } else {
+                        const float* sl = a.ws + (int64_t)(tile * S + o) * (WN * XM);
+#pragma unroll
+                        for (int u = 0; u < MT; ++u)
+                            v[u] = *reinterpret_cast<const f32x4*>(sl + (((wave * NT + s) * MT + u) * 64 + lane) * 4);
+                    }
+#pragma unroll
+                    for (int u = 0; u < MT; ++u) t[u] = o == 0 ? v[u] : t[u] + v[u];
                 }
+#pragma unroll
+                for (int u = 0; u < MT; ++u) acc[s][u] = t[u];
                 asm volatile("" ::: "memory");
             }
         }

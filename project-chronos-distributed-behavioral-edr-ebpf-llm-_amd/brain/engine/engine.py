@@ -41,6 +41,7 @@ import time
 from dataclasses import dataclass, field
 from typing import Any, Callable, Optional
 
+import numpy as np
 import torch
 
 from ... import ops
@@ -317,6 +318,7 @@ class Engine:
         self._snap_i = 0
         self._snap_seq = 0
         self._pending: Optional[_Snapshot] = None
+        self._ctx_need: Optional[int] = None  # _ctx_class's max(prompt + num_predict) over running rows
         self._deferred: list = []  # (request, reason) harvested, finished after the next launch (_flush_deferred)
         # cascade prefix state: device [P, block ids...] read by the decode graph, its O / lse scratch, host copy
         self._casc = None
@@ -542,6 +544,11 @@ class Engine:
     # scheduling
     # ------------------------------------------------------------------------------------------------------------
     def _admit(self) -> None:
+        if self.waiting and self._deferred:
+            # the KV blocks of requests the last harvest finished (their release is deferred past the GPU launch)
+            for r, _ in self._deferred:
+                self.blocks.release(r.blocks)
+                r.blocks = []
         if not self.prefilling and not self.running and self.cfg.prefill_ramp > 0:
             # Idle engine: nothing is queued on the GPU, so the host's tokenization of a whole chunk would be exposed
             # (~50 ms for 16k tokens of chains).  Start small and grow 4x per step, so admitting the next step's
@@ -813,6 +820,7 @@ class Engine:
             r.t_first = now
             self.prefilling.remove(r)
             self.running[r.slot] = r
+            self._ctx_need = None
             if "cancel_reason" in r.meta:  # cancelled mid-prefill: its blocks are computed now, drop it next step
                 self.cancel(r, r.meta["cancel_reason"])
 
@@ -947,7 +955,11 @@ class Engine:
         verdict contexts decode with one split (no combine) instead of the split count max_model_len would ask for
         (single stream, 512-token engine: 3.71 -> 3.64 ms/token; profiles/r2_single_stream_split_ab.json), and a
         128k request still gets its 64."""
-        need = max((len(r.prompt_ids) + r.num_predict for r in self.running.values()), default=1)
+        # cached between admissions: rows only leave the running set while nothing is admitted, and a stale (larger)
+        # bound only costs a split, so the 1024-row scan runs once per admission, not once per burst
+        if self._ctx_need is None:
+            self._ctx_need = max((len(r.prompt_ids) + r.num_predict for r in self.running.values()), default=1)
+        need = self._ctx_need
         c = 256
         while c < need:
             c *= 2
@@ -1038,17 +1050,25 @@ class Engine:
             self.phase_s["harvest_gpu_wait"] += time.perf_counter() - t
         # (snapshot slot, request) for requests still running as the same object (identity, not slot number)
         # (a request preempted after this snapshot was queued may be running again in another slot: its row here
-        # belongs to the run before the preemption)
-        live = [(s, r) for s, r in snap.owners.items()
-                if self.running.get(r.slot) is r and r.meta.get("preempt_seq", -1) < snap.seq]
-        if not live:
-            return []
-        st = snap.state[:snap.n].tolist()
-        nout, outs = snap.nout, snap.out
-        finished = [(s, r) for s, r in live if st[s] == DONE]
+        # belongs to the run before the preemption).  The snapshot is read through numpy views of its pinned buffers
+        # and only the rows that finished, parked or stream tokens get Python work: the full 1024-row scan and the
+        # per-row tensor indexing it replaced were ~1 ms of GPU-idle host time per burst on the 1024-stream wave
+        seq, owners, running = snap.seq, snap.owners, self.running
+
+        def alive(s: int) -> Optional[Request]:
+            r = owners.get(s)
+            if r is not None and running.get(r.slot) is r and r.meta.get("preempt_seq", -1) < seq:
+                return r
+            return None
+
+        st = snap.state[:snap.n].numpy()
+        nout, outs = snap.nout.numpy(), snap.out.numpy()
+        finished = [(s, r) for s in np.flatnonzero(st == DONE).tolist() if (r := alive(s)) is not None]
         # a parked row whose jump was already applied after this snapshot was queued (a mixed step harvests one step
         # late) is stale: applying its run again would rewind the row and duplicate the run
-        parked = [(s, r) for s, r in live if st[s] <= -2 and r.meta.get("jump_seq", 0) < snap.seq]
+        parked = [(s, r) for s in np.flatnonzero(st <= -2).tolist()
+                  if (r := alive(s)) is not None and r.meta.get("jump_seq", 0) < seq]
+        streaming = [(s, r) for s, r in owners.items() if r.meta.get("on_tokens") and alive(s) is not None]
         ended = {}  # slot -> output ids of jumped runs that end the verdict
         if parked:
             t = time.perf_counter()
@@ -1057,8 +1077,7 @@ class Engine:
         finished += [(s, r) for s, r in parked if s in ended]
         # (a jump's KV growth may have preempted some of these rows: they are queued again, not finished)
         finished = [(s, r) for s, r in finished if self.running.get(r.slot) is r]
-        live = [(s, r) for s, r in live if self.running.get(r.slot) is r]
-        streaming = [(s, r) for s, r in live if r.meta.get("on_tokens")]
+        streaming = [(s, r) for s, r in streaming if self.running.get(r.slot) is r]
         if not finished and not streaming:
             return []
         for s, r in streaming:  # incremental tokens for stream=true clients
@@ -1084,11 +1103,12 @@ class Engine:
             r.out_ids = r.resume_out + (ids[:-1] if stop else ids)
             r.t_done = now
             del self.running[r.slot]
-            self.blocks.release(r.blocks)
             reset.append(r.slot)
             self.free_slots.append(r.slot)
-            # detokenisation + the callback run after the next GPU launch (_flush_deferred): ~50 us per verdict, 50 ms
-            # of host time per 1024-chain wave that the GPU otherwise sat idle for between bursts
+            # KV block release, detokenisation and the callback run after the next GPU launch (_flush_deferred): ~60 us
+            # per verdict, ~60 ms of host time per 1024-chain wave that the GPU otherwise sat idle for between bursts.
+            # The row's slot is reset below, so no launch reads those blocks; they are free again before the next
+            # admission (every step flushes its deferred requests before it returns)
             self._deferred.append((r, "stop" if stop else "length"))
         self.free_slots.sort(reverse=True)  # lowest slot first keeps the decode bucket small
         idx = h2d(torch.tensor(reset, dtype=torch.int64), self.device)
@@ -1108,6 +1128,8 @@ class Engine:
             return []
         out, self._deferred = self._deferred, []
         for r, reason in out:
+            self.blocks.release(r.blocks)
+            r.blocks = []
             r.text = self.tok.decode(r.out_ids)
             self._finish(r, reason, timed=False)
         return [r for r, _ in out]
@@ -1129,7 +1151,7 @@ class Engine:
         every sampled token adds one to pos and nout), so after the run pos/ctx/nout/remaining all advance by k."""
         ended, unpark, rows = {}, [], []
         for s, r in parked:
-            state = -2 - st[s]
+            state = -2 - int(st[s])
             run, end = self.bank.jumps.get(state, ((), state))
             n0, k = int(nout[s]), len(run)
             if not run or n0 > self.cfg.max_out or n0 + k > self.cfg.max_out or \

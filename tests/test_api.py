@@ -227,8 +227,14 @@ def test_dp_router_failover_and_respawn():
             victim = router._procs[0].pid
             t_kill = time.perf_counter()
             os.kill(victim, signal.SIGKILL)
+            # the supervisor notices within a poll or two; under a loaded CPU (parallel test workers) allow a few
+            # seconds — the fresh worker is still importing / building its engine for far longer than that
             await asyncio.sleep(0.3)
-            ok_h, health = router.health()  # the fresh worker is still importing / building its engine
+            ok_h, health = router.health()
+            t_h = time.perf_counter()
+            while health["status"] == "ok" and time.perf_counter() - t_h < 5.0:
+                await asyncio.sleep(0.1)
+                ok_h, health = router.health()
             done = []
             for t in tasks:
                 done.append(await asyncio.wait_for(t, 600))  # the survivor runs 400-token requests on CPU

@@ -185,6 +185,10 @@ def test_decode_attention_rope_fused_matches_unfused(hq, hkv):
     """Batched decode step with RoPE + paged-KV write fused into the one-wave decode attention vs rope_kv_write +
     paged_attention (and the fp32 reference): ragged contexts incl. a new token at every block offset and past the
     64-entry block-table window; the caches must hold the same new K / V afterwards."""
+    _decode_rope_case(hq, hkv)
+
+
+def _decode_rope_case(hq, hkv):
     from chronos import ops
     from chronos.models.llama import get_config, rope_table
     from chronos.ops import reference as ref
