@@ -103,6 +103,23 @@ __device__ __forceinline__ void lg_dma16_asm(const void* base, int bytes, uint32
 constexpr int hb_wrow(int s, bool swiglu, int WN) { return swiglu ? (s < 4 ? 16 * s : WN / 2 + 16 * (s - 4)) : 16 * s; }
 // ... of 32-row block S (F8HB)
 constexpr int hb_wrow32(int S, bool swiglu, int WN) { return swiglu ? (S < 2 ? 32 * S : WN / 2 + 32 * (S - 2)) : 32 * S; }
+// HB bit 7 (HBV & 128): k-step 0 of a slab in growing-square order — MFMA (s, t) as soon as fa[s] and fb[t] can
+// have landed — with the set-0 reads alternating fa[0], fb[0], fb[1], fa[1], fb[2], fa[2], ...: the slab head's first
+// k MFMAs need ~2 sqrt(k) of the 16 reads issued at the end of the previous slab instead of k + 1, so fewer of them
+// wait on the tail of that read burst
+constexpr int hb_isqrt(int v) {
+    int n = 0;
+    while ((n + 1) * (n + 1) <= v) ++n;
+    return n;
+}
+constexpr int hb_sq_s(int ii) { return ii - hb_isqrt(ii) * hb_isqrt(ii) < hb_isqrt(ii) ? ii - hb_isqrt(ii) * hb_isqrt(ii) : hb_isqrt(ii); }
+constexpr int hb_sq_t(int ii) {
+    return ii - hb_isqrt(ii) * hb_isqrt(ii) < hb_isqrt(ii) ? hb_isqrt(ii) : ii - hb_isqrt(ii) * hb_isqrt(ii) - hb_isqrt(ii);
+}
+// set-0 read r of the alternating order: W (fa) or x (fb) block index; r = 0 -> fa[0], 1 -> fb[0], 2 n -> fb[n],
+// 2 n + 1 -> fa[n]
+constexpr bool hb_sq_isw(int r) { return r == 0 || (r >= 2 && (r & 1)); }
+constexpr int hb_sq_blk(int r) { return r < 2 ? 0 : r / 2; }
 // F8HB slab schedule (32 MFMA slots): x pieces spread over [B1, B2), W pieces over [B2, B3)
 constexpr int hb8_piece(int i, int B1, int B2, int B3, int NPW, int NPX) {
     for (int p = 0; p < NPX; ++p)
@@ -176,7 +193,7 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
     // W: 5 after B2 + 3 after B3, vmcnt(13)); bit 2 lgkmcnt(0) before the slab's last MFMA instead of hipcc's counted
     // waits at the next slab's head; bit 3 precomputed addressing (below); bit 4 LDS-staged epilogue; bit 5 the next
     // slab's reads from MFMA 94 (below)
-    constexpr bool HB = VAR >= 4 && VAR < 68;
+    constexpr bool HB = VAR >= 4 && VAR < 260;
     constexpr int HBV = HB ? VAR - 4 : 0;
     constexpr int ES = F8 ? 1 : 2;  // operand bytes per element
     // F8 + HB (VAR with bits 8 and 16: precomputed addressing, staged epilogue): the HB slab loop on
@@ -185,7 +202,13 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
                           (ST >= 3 ? VAR == 0 : (HB && (HBV & 24) == 24 && !(HBV & 2) && !(HBV & 32)))),
                   "fp8: ring schedule or the HB slab loop, 128-B rows, plain / SwiGLU epilogue");
     constexpr bool F8HB = F8 && HB;
-    constexpr bool L32 = M32 || F8HB;  // 32x32 accumulator blocks
+    // bit 6 (HBV & 64, bf16): the F8HB loop on v_mfma_f32_32x32x16_bf16 — a slot is two 16-deep MFMAs (the lo / hi
+    // 16 B of a 32-B fragment), so a slab is 32 slots of 64 MFMA cycles as in F8HB, with half the MFMA issues of
+    // the 16x16x32 loop
+    constexpr bool B32HB = HB && !F8 && (HBV & 64);
+    constexpr bool XHB = F8HB || B32HB;  // the 32-slot slab loop
+    static_assert(!B32HB || ((HBV & 24) == 24 && !(HBV & 2) && !(HBV & 32)), "32x32 HB: precomputed + staged");
+    constexpr bool L32 = M32 || XHB;  // 32x32 accumulator blocks
     using FT = std::conditional_t<F8, lg_i32x8, bf16x8>;  // MFMA operand fragment
     constexpr int NW = 2 * NWX;                       // waves: 2 along W x NWX along x (NWX = 4: two per SIMD)
     constexpr int RPI = 1024 / RB;                    // image rows per LDS-DMA instruction
@@ -424,9 +447,11 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
         // chunks 4 kk + 2 hf and + 1 of the 128-B image row, each one ds_read_b128 at its XOR-swizzled slot (chunk ^
         // (r & 7), as the DMA wrote it).  Both operands use the same (half, byte) -> k map.  One base VGPR per
         // (buffer parity, operand, k-step, half); block offsets are immediates.
-        lg_i32x8 ga0[F8HB ? NT / 2 : 1], gb0[F8HB ? MT / 2 : 1], ga1[F8HB ? NT / 2 : 1], gb1[F8HB ? MT / 2 : 1];
-        const unsigned char* f8b[F8HB ? 2 : 1][2][2][2];
-        if constexpr (F8HB) {
+        // (B32HB: a 32-deep k-step is two 16-deep MFMAs; lane half hf holds k 8 hf .. +7 of each, i.e. chunks
+        // 4 kk + hf (lo) and 4 kk + 2 + hf (hi))
+        lg_i32x8 ga0[XHB ? NT / 2 : 1], gb0[XHB ? MT / 2 : 1], ga1[XHB ? NT / 2 : 1], gb1[XHB ? MT / 2 : 1];
+        const unsigned char* f8b[XHB ? 2 : 1][2][2][2];
+        if constexpr (XHB) {
             const int r = lane & 31, hf = lane >> 5;
 #pragma unroll
             for (int p = 0; p < 2; ++p)
@@ -434,15 +459,15 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
                 for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
                     for (int h = 0; h < 2; ++h) {
-                        const int co = ((4 * kk + 2 * hf + h) ^ (r & 7)) << 4;
+                        const int co = ((F8 ? 4 * kk + 2 * hf + h : 4 * kk + 2 * h + hf) ^ (r & 7)) << 4;
                         f8b[p][0][kk][h] = smem + p * STAGE + (wrow32[0] + r) * RB + co;
                         f8b[p][1][kk][h] = smem + p * STAGE + WIMG + (xrow0 + r) * RB + co;
                     }
         }
         // one F8HB fragment: parity p, operand op (0 W, 1 x), k-step kk, block row offset off (bytes)
         auto f8rd = [&](int p, int op, int kk, int off) -> lg_i32x8 {
-            const lg_i32x4 lo = *reinterpret_cast<const lg_i32x4*>(f8b[F8HB ? p : 0][op][kk][0] + off);
-            const lg_i32x4 hi = *reinterpret_cast<const lg_i32x4*>(f8b[F8HB ? p : 0][op][kk][1] + off);
+            const lg_i32x4 lo = *reinterpret_cast<const lg_i32x4*>(f8b[XHB ? p : 0][op][kk][0] + off);
+            const lg_i32x4 hi = *reinterpret_cast<const lg_i32x4*>(f8b[XHB ? p : 0][op][kk][1] + off);
             return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
         };
         auto mm = [&](bf16x8 (&fa)[NT], bf16x8 (&fb)[MT]) {
@@ -476,12 +501,19 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
             lg_vmcnt<NPER>();  // slab 0 landed (slab 1 in flight)
         }
         lg_bar();
-        if constexpr (F8HB) {
+        if constexpr (XHB) {
             ga0[0] = f8rd(0, 0, 0, 0);  // (the loop's set-0 read order: ga[0], gb[*], ga[1..])
 #pragma unroll
             for (int u = 0; u < MT / 2; ++u) gb0[u] = f8rd(0, 1, 0, 32 * RB * u);
 #pragma unroll
             for (int s = 1; s < NT / 2; ++s) ga0[s] = f8rd(0, 0, 0, hb_wrow32(s, MODE == kSwiglu, WN) * RB);
+        } else if constexpr (HB && (HBV & 128)) {  // (the loop's alternating set-0 read order, see hb_sq_isw)
+#pragma unroll
+            for (int r = 0; r < NT + MT; ++r) {
+                const int b = hb_sq_blk(r);
+                if (hb_sq_isw(r)) fa0[b] = *reinterpret_cast<const bf16x8*>(smem + wrow0[b] * RB + loff[0]);
+                else fb0[b] = *reinterpret_cast<const bf16x8*>(smem + WIMG + (xrow0 + 16 * b) * RB + loff[0]);
+            }
         } else if constexpr (HB) {
             // the order of the loop's set-0 reads (fa[0], fb[*], fa[1..]): the same pending-read state enters the loop
             // from the prologue and from the back edge, so hipcc's waits at the first MFMAs stay counted
@@ -554,7 +586,7 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
             // the accumulators live in AGPRs across the whole loop: pinned at both ends, so the epilogue's VGPR use
             // (resid / SwiGLU / norm-scale forms) cannot make the register allocator shuffle them inside the loop
             auto pin_acc = [&]() {
-                if constexpr (F8HB) {
+                if constexpr (XHB) {
 #pragma unroll
                     for (int S = 0; S < NT / 2; ++S)
 #pragma unroll
@@ -567,7 +599,7 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
                 }
             };
             pin_acc();
-            if constexpr (F8HB) {
+            if constexpr (XHB) {
                 // W8A8 on the HB loop: a 128-B slab row is 128 e4m3 k = two 64-deep k-steps of 16
                 // v_mfma_scale_f32_32x32x64_f8f6f4 (4 W x 4 x blocks of 32, each MFMA 4x the issue time of a bf16
                 // 16x16x32), so a slab is 32 MFMA slots with the same per-slab bytes, fragment reads (2 ds_read_b128
@@ -618,12 +650,22 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
                                              ::"v"(isW ? vw : vx), "s"(r), "s"(q * pstride) : "memory");
                         }
                         constexpr int ii = i % MK, S = ii / (MT / 2), U = ii % (MT / 2);
-                        if constexpr (i < MK)
-                            acc32[S][U] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ga0[S], gb0[U], acc32[S][U], 0,
-                                                                                        0, 0, 127, 0, 127);
-                        else
-                            acc32[S][U] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(ga1[S], gb1[U], acc32[S][U], 0,
-                                                                                        0, 0, 127, 0, 127);
+                        const lg_i32x8& fa = i < MK ? ga0[S] : ga1[S];
+                        const lg_i32x8& fb = i < MK ? gb0[U] : gb1[U];
+                        if constexpr (F8)
+                            acc32[S][U] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa, fb, acc32[S][U], 0, 0, 0,
+                                                                                        127, 0, 127);
+                        else {  // B32HB: the two 16-deep halves
+                            typedef __bf16 lg_bf16x8 __attribute__((ext_vector_type(8)));
+                            acc32[S][U] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                                __builtin_bit_cast(lg_bf16x8, __builtin_shufflevector(fa, fa, 0, 1, 2, 3)),
+                                __builtin_bit_cast(lg_bf16x8, __builtin_shufflevector(fb, fb, 0, 1, 2, 3)), acc32[S][U], 0, 0,
+                                0);
+                            acc32[S][U] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                                __builtin_bit_cast(lg_bf16x8, __builtin_shufflevector(fa, fa, 4, 5, 6, 7)),
+                                __builtin_bit_cast(lg_bf16x8, __builtin_shufflevector(fb, fb, 4, 5, 6, 7)), acc32[S][U], 0, 0,
+                                0);
+                        }
                         if constexpr (i < MT / 2) gb1[i] = f8rd(P, 1, 1, 32 * RB * i);
                         if constexpr (i > F1 && (i - F1 - 1) % 2 == 0 && (i - F1 - 1) / 2 < NT / 2) {
                             constexpr int s = (i - F1 - 1) / 2;
@@ -702,7 +744,9 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
                                 asm volatile("s_add_u32 m0, m0, 0x400\n\tbuffer_load_dwordx4 %0, %1, %2 offen lds"
                                              ::"v"(isW ? vw : vx), "s"(r), "s"(q * pstride) : "memory");
                         }
-                        constexpr int ii = i % MFK, s = ii / MT, t = ii % MT;
+                        constexpr int ii = i % MFK;
+                        constexpr bool SQ = (HBV & 128) && i < MFK;  // (k-step 0 only: k-step 1's reads land early)
+                        constexpr int s = SQ ? hb_sq_s(ii) : ii / MT, t = SQ ? hb_sq_t(ii) : ii % MT;
                         if constexpr (i < MFK)
                             acc[s][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa0[s], fb0[t], acc[s][t], 0, 0, 0);
                         else
@@ -713,7 +757,13 @@ __global__ void __launch_bounds__(128 * NWX, 1) gemm_lg_kernel(PPArgs a) {
                             constexpr int r = (i - B1 - 1) / 3;
                             fa1[r] = *reinterpret_cast<const bf16x8*>(rbw[P][1] + hb_wrow(r, MODE == kSwiglu, WN) * RB);
                         }
-                        if constexpr (i >= B3 && (i - B3) % RSP == 0 && (i - B3) / RSP < NT + MT) {
+                        if constexpr ((HBV & 128) && i >= B3 && (i - B3) % RSP == 0 && (i - B3) / RSP < NT + MT) {
+                            constexpr int r = (i - B3) / RSP, b = hb_sq_blk(r);  // fa0, fb0, fb1, fa1, fb2, fa2, ...
+                            if constexpr (hb_sq_isw(r))
+                                fa0[b] = *reinterpret_cast<const bf16x8*>(rbw[1 - P][0] + hb_wrow(b, MODE == kSwiglu, WN) * RB);
+                            else
+                                fb0[b] = *reinterpret_cast<const bf16x8*>(rbx[1 - P][0] + 16 * RB * b);
+                        } else if constexpr (i >= B3 && (i - B3) % RSP == 0 && (i - B3) / RSP < NT + MT) {
                             constexpr int r = (i - B3) / RSP;  // fa[0], fb[0..MT-1], fa[1..NT-1]
                             if constexpr (r == 0) fa0[0] = *reinterpret_cast<const bf16x8*>(rbw[1 - P][0]);
                             else if constexpr (r <= MT)
@@ -1401,7 +1451,10 @@ void lg_launch(const PPArgs& a, hipStream_t st) {
     X(87, 256, 256, 128, 2, 2, 15) \
     X(88, 256, 256, 128, 2, 2, 29) \
     X(89, 256, 256, 128, 2, 2, 31) \
-    X(90, 256, 256, 128, 2, 2, 60)
+    X(90, 256, 256, 128, 2, 2, 60) \
+    X(91, 256, 256, 128, 2, 2, 93) \
+    X(92, 256, 256, 128, 2, 2, 157) \
+    X(93, 256, 256, 128, 2, 2, 159)
 
 template <int MODE, bool NORMP>
 bool lg_mode(int cfg, const PPArgs& a, hipStream_t st) {
@@ -1465,7 +1518,7 @@ int gemm_lg_xm(int cfg) {
         default: return 0;
     }
 }
-bool gemm_lg_splitk_ok(int cfg) { return cfg < 81 || cfg > 90 || cfg == 88 || cfg == 89 || cfg == 90; }
+bool gemm_lg_splitk_ok(int cfg) { return cfg < 81 || cfg > 93 || cfg >= 88; }
 
 int gemm_lg_wn(int cfg) {
     if (gemm_lg_ablations_built() && cfg >= 40 && cfg < 72) return 256;

@@ -20,7 +20,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-HB_CFGS = (88, 89)
+HB_CFGS = (88, 89, 92, 93)  # 92 / 93: 88 / 89 with the square k-step-0 order (HB bit 7)
 
 
 def t_us(fn, iters=8, rounds=5):
@@ -48,7 +48,11 @@ def main():
     ap.add_argument("--keys", default="", help="comma-separated 'N:K:mode' keys (default: every plan key)")
     ap.add_argument("--add-ms", default="", help="N:K:mode=M1/M2/.. rows to add before measuring (';'-separated)")
     ap.add_argument("--lib-margin", type=float, default=0.03)
+    ap.add_argument("--hb-cfgs", default=",".join(str(c) for c in HB_CFGS))
+    ap.add_argument("--own-only", action="store_true",
+                    help="never route a row to the library (rows whose in-situ fused epilogue the bare A/B misses)")
     a = ap.parse_args()
+    hb_cfgs = tuple(int(c) for c in a.hb_cfgs.split(",") if c)
     from chronos import ops
     from chronos.ops import gemm as G
 
@@ -90,9 +94,9 @@ def main():
             x = torch.randn(m, k, device=dev, generator=g).to(torch.bfloat16)
             r = torch.randn(m, n, device=dev, generator=g).to(torch.bfloat16) if mode == 2 else None
             cands = []
-            if row[1] >= 0 and row[1] not in HB_CFGS:
+            if row[1] >= 0 and row[1] not in hb_cfgs:
                 cands.append((row[1], row[2]))
-            for c in HB_CFGS:
+            for c in hb_cfgs:
                 if G._pp_valid(c, n, k, mode, 1, m):
                     cands.append((c, 1))
             rec = {"key": key, "M": m, "N": n, "K": k, "mode": mode, "was": row[1:]}
@@ -115,7 +119,7 @@ def main():
                 lf = lambda: torch.add(x @ w_next().t(), r)  # noqa: E731
             lib = t_us(lf)
             rec["lib_us"] = round(lib, 1)
-            if best is None or lib * (1 + a.lib_margin) < best[0]:
+            if best is None or (not a.own_only and lib * (1 + a.lib_margin) < best[0]):
                 row[1], row[2] = -1, 1
             else:
                 row[1], row[2] = best[1], best[2]
