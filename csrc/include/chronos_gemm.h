@@ -37,7 +37,7 @@ constexpr int kLGConfigs = 28;
 // N = 6144, M = 1024 — one round on 256 CUs) and 78-79 (32-row x tiles with 7 / 12-stage rings: mid-M weight streams
 // are bound by the W bytes in flight per CU, so nearly all of the 160 KiB LDS holds W stages) and 80 (cfg 20's slab
 // schedule on 32x32x16 MFMAs) and 81-90 (4 waves, 128 x 128 per wave, the three-barrier slab loop: VAR 4-60 in gemm_lg.hip)
-constexpr int kLGTinyFirst = 72, kLGTinyConfigs = 22;
+constexpr int kLGTinyFirst = 72, kLGTinyConfigs = 23;
 int gemm_lg_xm(int cfg);  // x rows per tile
 int gemm_lg_wn(int cfg);  // W rows per tile
 bool gemm_lg_splitk_ok(int cfg);  // false for the HB configs (VAR 4): no split-K path

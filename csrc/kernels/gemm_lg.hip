@@ -1454,7 +1454,8 @@ void lg_launch(const PPArgs& a, hipStream_t st) {
     X(90, 256, 256, 128, 2, 2, 60) \
     X(91, 256, 256, 128, 2, 2, 93) \
     X(92, 256, 256, 128, 2, 2, 157) \
-    X(93, 256, 256, 128, 2, 2, 159)
+    X(93, 256, 256, 128, 2, 2, 159) \
+    X(94, 256, 256, 128, 2, 2, 189)
 
 template <int MODE, bool NORMP>
 bool lg_mode(int cfg, const PPArgs& a, hipStream_t st) {
@@ -1518,7 +1519,7 @@ int gemm_lg_xm(int cfg) {
         default: return 0;
     }
 }
-bool gemm_lg_splitk_ok(int cfg) { return cfg < 81 || cfg > 93 || cfg >= 88; }
+bool gemm_lg_splitk_ok(int cfg) { return cfg < 81 || cfg > 94 || cfg >= 88; }
 
 int gemm_lg_wn(int cfg) {
     if (gemm_lg_ablations_built() && cfg >= 40 && cfg < 72) return 256;

@@ -41,13 +41,14 @@ _PP_BM = {0: 256, 1: 128, 2: 256, 3: 128, 4: 256, 5: 128, 6: 256, 7: 128, 8: 256
           12: 256, 13: 128, 14: 256, 15: 128, 16: 256, 17: 128, 18: 256, 19: 128, 20: 256, 21: 256, 22: 128, 23: 128,
           24: 256, 25: 128, 26: 256, 27: 128, 28: 128, 29: 128, 30: 256, 31: 128, 32: 128, 33: 64, 34: 128, 35: 256,
           36: 64, 37: 128, 38: 64, 39: 64, 72: 32, 73: 32, 74: 32, 75: 32, 76: 128, 77: 128, 78: 32, 79: 32, 80: 256,
-          **{c: 256 for c in range(81, 94)}}
+          **{c: 256 for c in range(81, 95)}}
 _PP_BN = {0: 256, 1: 256, 2: 128, 3: 128, 4: 256, 5: 256, 6: 128, 7: 128, 8: 256, 9: 256, 10: 128, 11: 128,
           12: 256, 13: 256, 14: 128, 15: 128, 16: 256, 17: 256, 18: 128, 19: 128, 20: 256, 21: 256, 22: 256, 23: 128,
           24: 256, 25: 256, 26: 256, 27: 256, 28: 128, 29: 256, 30: 128, 31: 128, 32: 64, 33: 64, 34: 64, 35: 64, 36: 64, 37: 64, 38: 128, 39: 64, 72: 64, 73: 128, 74: 64, 75: 128, 76: 192, 77: 192, 78: 128, 79: 64, 80: 256,
-          **{c: 256 for c in range(81, 94)}}
-HB_FIRST, HB_LAST = 81, 93  # gemm_lg.hip HB configs (91: the 32x32x16 MFMA form; 92 / 93: 88 / 89 + square order)
-HB_SPLITK = (88, 89, 90, 91, 92, 93)  # ... with the staged epilogue: the only ones with a split-K path
+          **{c: 256 for c in range(81, 95)}}
+HB_FIRST, HB_LAST = 81, 94  # gemm_lg.hip HB configs (91: the 32x32x16 MFMA form; 92 / 93: 88 / 89 + square order;
+# 94: 92 + the set-0 reads from MFMA 94)
+HB_SPLITK = (88, 89, 90, 91, 92, 93, 94)  # ... with the staged epilogue: the only ones with a split-K path
 LG_FIRST = 12  # first gemm_lg.hip config: kResid partials every BN/2 columns (gemm_pp: BN/4)
 # relative per-CU MAC rate of each tile config at full occupancy (gate_up M = 1024 / 16384 sweeps, profiles/r3_gemm_pp_*,
 # profiles/r4_gemm_lg_*)
@@ -56,7 +57,7 @@ _PP_RATE = {0: 1.0, 1: 0.84, 2: 0.84, 3: 0.66, 4: 1.0, 5: 0.71, 6: 0.73, 7: 0.6,
             23: 0.75, 24: 1.1, 25: 0.8, 26: 1.1, 27: 0.8, 28: 0.75, 29: 0.8, 30: 0.8, 31: 0.75, 32: 0.5,
             33: 0.4, 34: 0.5, 35: 0.55, 36: 0.4, 37: 0.5, 38: 0.5, 39: 0.4, 72: 0.3,
             73: 0.3, 74: 0.3, 75: 0.3, 76: 0.75, 77: 0.7, 78: 0.3, 79: 0.3, 80: 1.05,
-            **{c: 1.15 for c in range(81, 94)}}
+            **{c: 1.15 for c in range(81, 95)}}
 # skinny-M configs (gemm_skinny.hip SK_CONFIGS): plan id SK_BASE + c -> (RT: W tiles of 16 rows, MT: M <= 16 MT,
 # NW: waves splitting K inside the workgroup)
 SK_BASE = 100
