@@ -45,6 +45,9 @@ def main():
     ap.add_argument("--out-plan", default=None)
     ap.add_argument("--out-table", default=None)
     ap.add_argument("--min-m", type=int, default=512)
+    ap.add_argument("--max-m", type=int, default=1 << 30)
+    ap.add_argument("--extra-cfgs", default="",
+                    help="more candidates for every row, 'cfg/splitk' comma-separated (e.g. 19/1,30/2)")
     ap.add_argument("--keys", default="", help="comma-separated 'N:K:mode' keys (default: every plan key)")
     ap.add_argument("--add-ms", default="", help="N:K:mode=M1/M2/.. rows to add before measuring (';'-separated)")
     ap.add_argument("--lib-margin", type=float, default=0.03)
@@ -53,6 +56,7 @@ def main():
                     help="never route a row to the library (rows whose in-situ fused epilogue the bare A/B misses)")
     a = ap.parse_args()
     hb_cfgs = tuple(int(c) for c in a.hb_cfgs.split(",") if c)
+    extra = [tuple(int(v) for v in c.split("/")) for c in a.extra_cfgs.split(",") if c]
     from chronos import ops
     from chronos.ops import gemm as G
 
@@ -76,7 +80,7 @@ def main():
     for key in keys:
         n, k, mode = (int(v) for v in key.split(","))
         rows = rows_by_key[key]
-        todo = [r for r in rows if r[0] >= a.min_m]
+        todo = [r for r in rows if a.min_m <= r[0] <= a.max_m]
         if not todo:
             continue
         wb = n * k * 2
@@ -99,6 +103,9 @@ def main():
             for c in hb_cfgs:
                 if G._pp_valid(c, n, k, mode, 1, m):
                     cands.append((c, 1))
+            for c, sk in extra:
+                if (c, sk) not in cands and G._pp_valid(c, n, k, mode, sk, m):
+                    cands.append((c, sk))
             rec = {"key": key, "M": m, "N": n, "K": k, "mode": mode, "was": row[1:]}
             best = None
             for cfg, sk in cands:
