@@ -192,6 +192,7 @@ def main():
     from chronos.parallel.tp import TPContext
     from chronos.sensor.prompt import VERDICT_SCHEMA, build_prompt
     from chronos.sensor.replay import synthetic_chains
+    from chronos.utils import freeze_startup_objects
 
     tp = TPContext.single()
     if a.tp > 1:
@@ -214,6 +215,7 @@ def main():
     # TP: the ranks of a replica submit the same chains in the same order and step the same deterministic scheduler,
     # so they stay in lockstep by construction (the serving path adds the leader broadcast of parallel/tp_engine.py)
     eng = Engine(cfg, tp=tp)
+    freeze_startup_objects()  # no ~100 ms full-GC stalls inside the timed waves (profiles/r6/gc_pause.txt)
     total_steps = a.warmup + a.steps
     per_stream = total_steps if a.mode == "wave" else 2 * total_steps + 2  # closed loop: fast streams cycle more
     closed_warm = 2  # closed-loop warmup steps (the prefix cache and decode buckets settle)
@@ -253,8 +255,11 @@ def main():
         t0 = time.perf_counter()
         timed = []
         for s in range(a.warmup, total_steps):
+            ts, ph0 = time.perf_counter(), dict(eng.phase_s)
             timed += run_step(prompts[s * a.streams:(s + 1) * a.streams])
-            progress(f"step {s} done")
+            # per-step wall time and host phase split (diagnostics; the timed region is still t0 .. the barrier below)
+            dph = {k: round(v - ph0.get(k, 0.0), 3) for k, v in eng.phase_s.items()}
+            progress(f"step {s} done {time.perf_counter() - ts:.3f}s {json.dumps(dph)}")
         barrier()
         elapsed = time.perf_counter() - t0
         hits = eng.stats["prefix_hit_tokens"] - hit0

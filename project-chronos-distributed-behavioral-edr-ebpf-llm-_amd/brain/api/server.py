@@ -23,6 +23,7 @@ import time
 
 from aiohttp import web
 
+from ...utils import freeze_startup_objects
 from ...utils.metrics import METRICS
 from .protocol import (OLLAMA_VERSION, BadRequest, GenerateParams, StopFilter, apply_stop, chat_response,
                        stop_context_ids,
@@ -269,6 +270,7 @@ def main(argv=None) -> int:
                 raise SystemExit(f"world size {grp.world} != {'--tp' if a.tp > 1 else '--cp'} {want}")
             tpe = TPEngine(cfg, grp, ctrl) if a.tp > 1 else TPEngine(cfg, TPContext.single(), ctrl, cp=grp)
             if grp.rank != 0:
+                freeze_startup_objects()
                 tpe.follower_loop()  # until the leader shuts down
                 return 0
             def fatal(e):  # the group is out of lockstep: exit non-zero so the supervisor restarts every rank
@@ -284,6 +286,7 @@ def main(argv=None) -> int:
             from .service import EngineService
 
             backend = EngineService.from_config(cfg, a.served_name)
+    freeze_startup_objects()  # after the engine is built: no full-GC walks over start-up objects
     app = make_app(backend, a.served_name, a.request_timeout or None)
     web.run_app(app, host=a.host, port=a.port, access_log=None)
     return 0

@@ -43,6 +43,7 @@ def _worker(rank: int, cfg_dict: dict, req_q, res_q, device: str, fail_start: bo
 
     from ..brain.api.protocol import GenerateParams, chat_prompt_ids
     from ..brain.engine.engine import Engine, EngineConfig
+    from ..utils import freeze_startup_objects
 
     if device == "cuda":
         torch.cuda.set_device(rank)
@@ -50,6 +51,7 @@ def _worker(rank: int, cfg_dict: dict, req_q, res_q, device: str, fail_start: bo
     else:  # CPU replicas share the host: split its cores instead of each oversubscribing all of them
         torch.set_num_threads(max(1, (os.cpu_count() or 1) // max(1, replicas)))
     eng = Engine(EngineConfig(**cfg_dict))
+    freeze_startup_objects()  # the replica process is an entry point of its own
     res_q.put(("ready", rank, None))
 
     def finish(rid):
